@@ -1,0 +1,176 @@
+/*
+ * prio3gpu.h -- C ABI of the MI355X (gfx950) batched Prio3 preparation + aggregation engine.
+ *
+ * This is the drop-in boundary for Janus's leader/helper aggregate-init hot path.  The reference
+ * (Janus 0.6, DAP-07) calls prio 0.15.1's `prio::vdaf::Aggregator` trait ONE REPORT AT A TIME:
+ *
+ *   trait Aggregator<16, 16>            (prio 0.15.1 src/vdaf.rs; surface mirrored by the fake VDAF
+ *                                        at core/src/test_util/dummy_vdaf.rs:80-141)
+ *     prepare_init(verify_key, agg_id, &(), nonce, public_share, input_share)
+ *         -> (PrepareState, PrepareShare)                       -> prio3gpu_prepare_init
+ *     prepare_shares_to_prepare_message(&(), [PrepareShare; 2])
+ *         -> PrepareMessage                                     -> prio3gpu_prepare_shares_to_prepare_message
+ *     prepare_next(PrepareState, PrepareMessage)
+ *         -> PrepareTransition::Finish(OutputShare)             -> prio3gpu_prepare_next
+ *     aggregate(&(), impl IntoIterator<OutputShare>) -> AggregateShare
+ *   Aggregatable::{merge, accumulate}  (dummy_vdaf.rs:230-242)  -> prio3gpu_prepare_next(agg != NULL),
+ *                                                                  prio3gpu_agg_merge_bytes
+ *   Collector::unshard (collector/src/lib.rs:539)               -> prio3gpu_agg_read + host sum
+ *
+ * called from
+ *   helper  aggregator/src/aggregator.rs:1775-1797   helper_initialized + evaluate + accumulate
+ *                                                    -> prio3gpu_helper_init (fused, whole job)
+ *   leader  aggregator/src/aggregator/aggregation_job_driver.rs:362-380   leader_initialized
+ *                                                    -> prio3gpu_prepare_init(agg_id = 0)
+ *           aggregation_job_driver.rs:579-627         leader_continued + accumulate
+ *                                                    -> prio3gpu_prepare_next(agg != NULL)
+ *   accumulate aggregator/src/aggregator/accumulator.rs:76-122  (per batch identifier)
+ *   VDAF construction aggregator/src/aggregator.rs:797-840 (TaskAggregator::new)
+ *                                                    -> prio3gpu_ctx_create
+ *
+ * Every batch entry point takes n reports.  Buffers hold the DAP/VDAF little-endian encodings,
+ * report-major (report r at base + r * <len>).  They may be HOST or DEVICE pointers (detected);
+ * device pointers avoid all PCIe traffic.  Errors never fail a whole batch for one report:
+ * per-report status bytes mirror DAP `PrepareError` (messages/src/lib.rs:2288-2298):
+ *   0 = ok, 5 = VdafPrepError, 8 = InvalidMessage.  A report whose status is non-zero on entry to
+ * a later stage is skipped by that stage (its outputs are left as zeros).
+ * Return codes: 0 = ok, < 0 = API error (bad argument, HIP failure).
+ *
+ * Thread safety: one context may be used by one thread at a time; create one context per
+ * concurrent job driver (each context owns its own HIP stream).
+ */
+#ifndef PRIO3GPU_H
+#define PRIO3GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* VDAF kinds (VdafInstance, core/src/task.rs:24-59).  Prio3CountVec{length} is
+ * SUMVEC with bits = 1 (aggregator.rs:805-813). */
+enum prio3gpu_kind {
+  PRIO3GPU_COUNT = 0,     /* Prio3Count                     Field64  */
+  PRIO3GPU_SUM = 1,       /* Prio3Sum { bits }               Field128 */
+  PRIO3GPU_SUMVEC = 2,    /* Prio3SumVec { bits, length, chunk_length }  Field128 */
+  PRIO3GPU_HISTOGRAM = 3  /* Prio3Histogram { length, chunk_length }     Field128 */
+};
+
+enum prio3gpu_status {
+  PRIO3GPU_OK = 0,
+  PRIO3GPU_VDAF_PREP_ERROR = 5,
+  PRIO3GPU_INVALID_MESSAGE = 8
+};
+
+enum prio3gpu_err {
+  PRIO3GPU_E_OK = 0,
+  PRIO3GPU_E_ARG = -1,
+  PRIO3GPU_E_HIP = -2,
+  PRIO3GPU_E_RCCL = -3,
+  PRIO3GPU_E_CAPACITY = -4
+};
+
+typedef struct prio3gpu_ctx prio3gpu_ctx;
+typedef struct prio3gpu_state prio3gpu_state;
+typedef struct prio3gpu_agg prio3gpu_agg;
+typedef struct prio3gpu_comm prio3gpu_comm;
+
+/* Sizes of the encodings for a configured context. */
+typedef struct prio3gpu_sizes {
+  uint32_t field_size;          /* 8 (Field64) or 16 (Field128) */
+  uint32_t meas_len;            /* measurement-share length (field elements) */
+  uint32_t proof_len;           /* proof-share length */
+  uint32_t verifier_len;
+  uint32_t joint_rand_len;
+  uint32_t output_len;
+  uint32_t leader_input_share;  /* bytes: meas || proof || [blind] */
+  uint32_t helper_input_share;  /* bytes: meas seed || proof seed || [blind] */
+  uint32_t public_share;        /* bytes: [part_0 || part_1] */
+  uint32_t prep_share;          /* bytes: verifier || [part] */
+  uint32_t prep_msg;            /* bytes: [joint rand seed] */
+  uint32_t aggregate_share;     /* bytes: output_len * field_size */
+} prio3gpu_sizes;
+
+/* Prio3::new_{count,sum,sum_vec,histogram}(2, ...) + verify key (aggregator.rs:797-840).
+ * `bits`, `length`, `chunk_length` are ignored where the kind does not use them.
+ * `device` = HIP device ordinal. */
+int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,
+                        const uint8_t verify_key[16], int device, prio3gpu_ctx** out);
+int prio3gpu_ctx_destroy(prio3gpu_ctx* ctx);
+int prio3gpu_ctx_sizes(const prio3gpu_ctx* ctx, prio3gpu_sizes* out);
+/* Wait for all work queued on the context's stream. */
+int prio3gpu_ctx_sync(prio3gpu_ctx* ctx);
+/* The context's HIP stream (hipStream_t), for callers that interoperate (e.g. bench timing). */
+void* prio3gpu_ctx_stream(prio3gpu_ctx* ctx);
+
+/* Preparation state + device scratch for up to `capacity` reports of one aggregator
+ * (Prio3PrepareState for a whole batch). */
+int prio3gpu_state_create(prio3gpu_ctx* ctx, int agg_id, size_t capacity, prio3gpu_state** out);
+int prio3gpu_state_destroy(prio3gpu_state* st);
+
+/* Aggregate shares: `num_slots` batch identifiers (caller maps BatchIdentifier -> slot). */
+int prio3gpu_agg_create(prio3gpu_ctx* ctx, uint32_t num_slots, prio3gpu_agg** out);
+int prio3gpu_agg_destroy(prio3gpu_agg* agg);
+int prio3gpu_agg_reset(prio3gpu_agg* agg);
+/* Read one slot's aggregate share (aggregate_share bytes) and report count. */
+int prio3gpu_agg_read(prio3gpu_agg* agg, uint32_t slot, uint8_t* out_share, uint64_t* out_count);
+/* Aggregatable::merge: slot += share (aggregate_share bytes, host or device), count += count. */
+int prio3gpu_agg_merge_bytes(prio3gpu_agg* agg, uint32_t slot, const uint8_t* share,
+                             uint64_t count);
+
+/* prepare_init for n reports with the state's agg_id (0 = leader, 1 = helper).
+ *   nonces          n x 16          (report IDs)
+ *   public_shares   n x public_share
+ *   input_shares    n x (agg_id == 0 ? leader_input_share : helper_input_share)
+ *   out_prep_shares n x prep_share   (may be NULL: kept only inside the state)
+ *   status          n bytes, in/out (initialise to 0)
+ * The leader's input shares must stay valid (unchanged) until prio3gpu_prepare_next on the same
+ * state when they are DEVICE pointers; host inputs are copied into the state. */
+int prio3gpu_prepare_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const uint8_t* nonces,
+                          const uint8_t* public_shares, const uint8_t* input_shares,
+                          uint8_t* out_prep_shares, uint8_t* status);
+
+/* prepare_shares_to_prepare_message for n reports (leader share, helper share) -> prep msg. */
+int prio3gpu_prepare_shares_to_prepare_message(prio3gpu_ctx* ctx, size_t n,
+                                               const uint8_t* leader_prep_shares,
+                                               const uint8_t* helper_prep_shares,
+                                               uint8_t* out_prep_msgs, uint8_t* status);
+
+/* prepare_next for the n reports prepared in `st`: check prep msg == corrected joint-rand seed;
+ * optionally write output shares (n x aggregate_share bytes) and/or accumulate into `agg` at
+ * `batch_slots[r]` (NULL slots = slot 0).  Reports with non-zero status are not accumulated. */
+int prio3gpu_prepare_next(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const uint8_t* prep_msgs,
+                          uint8_t* status, uint8_t* out_output_shares, const uint32_t* batch_slots,
+                          prio3gpu_agg* agg);
+
+/* Helper aggregate-init, fused (aggregator.rs:1613-1848 for a whole job): prepare_init(1) +
+ * prepare_shares_to_prepare_message(leader share, own share) + prepare_next + accumulate.
+ * Writes the prep msg each report's Finish message carries. */
+int prio3gpu_helper_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const uint8_t* nonces,
+                         const uint8_t* public_shares, const uint8_t* helper_input_shares,
+                         const uint8_t* leader_prep_shares, const uint32_t* batch_slots,
+                         uint8_t* out_prep_msgs, uint8_t* status, prio3gpu_agg* agg);
+
+/* Multi-GPU merge of per-GPU partial aggregates (one process per GPU).  RCCL all-gather of the
+ * raw field-element bytes over xGMI, then a mod-p add kernel (RCCL sum is neither modular nor
+ * 128-bit).  Counts are summed with an RCCL uint64 all-reduce. */
+int prio3gpu_comm_unique_id(uint8_t out_id[128]);
+int prio3gpu_comm_init(const uint8_t id[128], int nranks, int rank, int device,
+                       prio3gpu_comm** out);
+int prio3gpu_comm_destroy(prio3gpu_comm* comm);
+int prio3gpu_agg_allreduce(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg* agg);
+
+/* Device memory helpers (bench / tests that stage inputs in HBM without torch). */
+int prio3gpu_dev_alloc(prio3gpu_ctx* ctx, size_t bytes, void** out);
+int prio3gpu_dev_free(prio3gpu_ctx* ctx, void* p);
+int prio3gpu_memcpy(prio3gpu_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* Last error message for this thread (static storage). */
+const char* prio3gpu_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRIO3GPU_H */

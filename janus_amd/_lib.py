@@ -1,0 +1,114 @@
+"""Loader for the in-tree HIP library `janus_amd/lib/libprio3gpu.so` (C ABI: include/prio3gpu.h).
+
+There is no CPU fallback: if the library is missing or cannot be loaded, every entry point raises.
+Build it with `python -c "import __graft_entry__ as g; g.build()"` (hipcc, gfx950).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+LIB_DIR = ROOT / "lib"
+LIB_PATH = LIB_DIR / "libprio3gpu.so"
+CSRC = ROOT / "csrc"
+INCLUDE = ROOT.parent / "include"
+
+_lib = None
+
+
+class Prio3GpuError(RuntimeError):
+    pass
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the HIP engine for gfx950 into janus_amd/lib/libprio3gpu.so."""
+    srcs = [CSRC / "engine.hip"]
+    deps = srcs + list(CSRC.glob("*.h")) + [INCLUDE / "prio3gpu.h"]
+    if LIB_PATH.exists() and not force:
+        newest = max(p.stat().st_mtime for p in deps)
+        if LIB_PATH.stat().st_mtime >= newest:
+            return LIB_PATH
+    LIB_DIR.mkdir(exist_ok=True)
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-o", str(tmp), str(srcs[0]), "-lrccl"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def _declare(lib):
+    c = ctypes
+    P = c.c_void_p
+    u8p = c.c_void_p
+    sigs = {
+        "prio3gpu_ctx_create": (c.c_int, [c.c_int, c.c_uint32, c.c_uint32, c.c_uint32, c.c_char_p,
+                                          c.c_int, c.POINTER(P)]),
+        "prio3gpu_ctx_destroy": (c.c_int, [P]),
+        "prio3gpu_ctx_sizes": (c.c_int, [P, P]),
+        "prio3gpu_ctx_sync": (c.c_int, [P]),
+        "prio3gpu_ctx_stream": (P, [P]),
+        "prio3gpu_state_create": (c.c_int, [P, c.c_int, c.c_size_t, c.POINTER(P)]),
+        "prio3gpu_state_destroy": (c.c_int, [P]),
+        "prio3gpu_agg_create": (c.c_int, [P, c.c_uint32, c.POINTER(P)]),
+        "prio3gpu_agg_destroy": (c.c_int, [P]),
+        "prio3gpu_agg_reset": (c.c_int, [P]),
+        "prio3gpu_agg_read": (c.c_int, [P, c.c_uint32, u8p, c.POINTER(c.c_uint64)]),
+        "prio3gpu_agg_merge_bytes": (c.c_int, [P, c.c_uint32, u8p, c.c_uint64]),
+        "prio3gpu_prepare_init": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, u8p, u8p]),
+        "prio3gpu_prepare_shares_to_prepare_message": (c.c_int, [P, c.c_size_t, u8p, u8p, u8p, u8p]),
+        "prio3gpu_prepare_next": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, P, P]),
+        "prio3gpu_helper_init": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, u8p, P, u8p, u8p, P]),
+        "prio3gpu_comm_unique_id": (c.c_int, [u8p]),
+        "prio3gpu_comm_init": (c.c_int, [u8p, c.c_int, c.c_int, c.c_int, c.POINTER(P)]),
+        "prio3gpu_comm_destroy": (c.c_int, [P]),
+        "prio3gpu_agg_allreduce": (c.c_int, [P, P, P]),
+        "prio3gpu_dev_alloc": (c.c_int, [P, c.c_size_t, c.POINTER(P)]),
+        "prio3gpu_dev_free": (c.c_int, [P, P]),
+        "prio3gpu_memcpy": (c.c_int, [P, P, P, c.c_size_t]),
+        "prio3gpu_last_error": (c.c_char_p, []),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return sigs
+
+
+# Every symbol include/prio3gpu.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "prio3gpu_ctx_create", "prio3gpu_ctx_destroy", "prio3gpu_ctx_sizes", "prio3gpu_ctx_sync",
+    "prio3gpu_ctx_stream", "prio3gpu_state_create", "prio3gpu_state_destroy",
+    "prio3gpu_agg_create", "prio3gpu_agg_destroy", "prio3gpu_agg_reset", "prio3gpu_agg_read",
+    "prio3gpu_agg_merge_bytes", "prio3gpu_prepare_init",
+    "prio3gpu_prepare_shares_to_prepare_message", "prio3gpu_prepare_next", "prio3gpu_helper_init",
+    "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
+    "prio3gpu_agg_allreduce", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
+    "prio3gpu_last_error",
+]
+
+
+def lib():
+    """The loaded HIP library; raises Prio3GpuError when it is absent (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise Prio3GpuError(f"HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+        try:
+            l = ctypes.CDLL(str(LIB_PATH))
+        except OSError as e:
+            raise Prio3GpuError(f"cannot load {LIB_PATH}: {e}") from e
+        _declare(l)
+        _lib = l
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().prio3gpu_last_error().decode(errors="replace")
+        raise Prio3GpuError(f"{what} failed ({rc}): {msg}")

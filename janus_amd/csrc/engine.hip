@@ -1,0 +1,925 @@
+// Host side of the prio3gpu C ABI (include/prio3gpu.h): contexts, batch states, aggregates,
+// kernel launches and the RCCL merge.  One HIP stream per context.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/prio3gpu.h"
+#include "prio3_kernels.h"
+
+using namespace p3g;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      set_err("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return PRIO3GPU_E_HIP;                                                      \
+    }                                                                             \
+  } while (0)
+
+#define RCCLCHK(x)                                                                  \
+  do {                                                                              \
+    ncclResult_t e_ = (x);                                                          \
+    if (e_ != ncclSuccess) {                                                        \
+      set_err("%s failed: %s (%s:%d)", #x, ncclGetErrorString(e_), __FILE__, __LINE__); \
+      return PRIO3GPU_E_RCCL;                                                       \
+    }                                                                               \
+  } while (0)
+
+#define CHK(x)                   \
+  do {                           \
+    int rc_ = (x);               \
+    if (rc_ != 0) return rc_;    \
+  } while (0)
+
+typedef unsigned __int128 u128;
+
+// ---- host modular arithmetic for table setup only ---------------------------------------------
+u128 addmod(u128 x, u128 y, u128 p) {
+  u128 s = x + y;
+  if (s < x || s >= p) s -= p;
+  return s;
+}
+u128 mulmod(u128 a, u128 b, u128 p) {
+  u128 r = 0;
+  a %= p;
+  while (b) {
+    if (b & 1) r = addmod(r, a, p);
+    a = addmod(a, a, p);
+    b >>= 1;
+  }
+  return r;
+}
+u128 powmod(u128 a, u128 e, u128 p) {
+  u128 r = 1;
+  while (e) {
+    if (e & 1) r = mulmod(r, a, p);
+    a = mulmod(a, a, p);
+    e >>= 1;
+  }
+  return r;
+}
+const u128 P128 = ((u128)0xFFFFFFFFFFFFFFE4ull << 64) | 1u;
+const u128 P64 = (u128)0xFFFFFFFF00000001ull;
+
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice;
+}
+
+uint32_t next_pow2(uint32_t x) {
+  uint32_t r = 1;
+  while (r < x) r <<= 1;
+  return r;
+}
+uint32_t ilog2(uint32_t x) {
+  uint32_t l = 0;
+  while ((1u << l) < x) ++l;
+  return l;
+}
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    HIPCHK(hipMalloc(&p, bytes ? bytes : 16));
+    cap = bytes;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+
+}  // namespace
+
+struct prio3gpu_ctx {
+  Cfg cfg{};
+  prio3gpu_sizes sz{};
+  uint8_t vk[16];
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevBuf twiddles;
+  // generic staging (inputs given as host pointers) and scratch
+  DevBuf io[6];
+  DevBuf perm, chunks, partials, pcounts;
+  std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
+};
+
+struct prio3gpu_state {
+  prio3gpu_ctx* ctx = nullptr;
+  int agg_id = 0;
+  size_t cap = 0;
+  size_t n = 0;
+  DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input;
+  CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
+};
+
+struct prio3gpu_agg {
+  prio3gpu_ctx* ctx = nullptr;
+  uint32_t slots = 0;
+  DevBuf share;   // slots x out_len x ES
+  DevBuf counts;  // slots x u64
+};
+
+struct prio3gpu_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  DevBuf gather, cgather;
+};
+
+namespace {
+
+int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_t chunk) {
+  Cfg& g = c->cfg;
+  g.kind = (uint32_t)kind;
+  g.algo_id = (uint32_t)kind;  // Count 0, Sum 1, SumVec 2, Histogram 3 (VDAF-07 algorithm IDs)
+  uint32_t calls = 0, arity = 0, prove_rand = 0;
+  switch (kind) {
+    case PRIO3GPU_COUNT:
+      g.es = 8;
+      g.meas_len = 1;
+      g.out_len = 1;
+      g.jr_len = 0;
+      calls = 1;
+      arity = 2;
+      prove_rand = 2;
+      break;
+    case PRIO3GPU_SUM:
+      if (bits == 0 || bits > 64) {
+        set_err("Prio3Sum: bits must be in 1..64");
+        return PRIO3GPU_E_ARG;
+      }
+      g.es = 16;
+      g.meas_len = bits;
+      g.out_len = 1;
+      g.jr_len = 1;
+      calls = bits;
+      arity = 1;
+      prove_rand = 1;
+      break;
+    case PRIO3GPU_SUMVEC:
+      if (bits == 0 || bits > 64 || length == 0 || chunk == 0) {
+        set_err("Prio3SumVec: bad parameters");
+        return PRIO3GPU_E_ARG;
+      }
+      g.es = 16;
+      g.meas_len = bits * length;
+      g.out_len = length;
+      g.jr_len = 1;
+      calls = (g.meas_len + chunk - 1) / chunk;
+      arity = 2 * chunk;
+      prove_rand = 2 * chunk;
+      break;
+    case PRIO3GPU_HISTOGRAM:
+      if (length == 0 || chunk == 0) {
+        set_err("Prio3Histogram: bad parameters");
+        return PRIO3GPU_E_ARG;
+      }
+      g.es = 16;
+      g.meas_len = length;
+      g.out_len = length;
+      g.jr_len = 2;
+      calls = (length + chunk - 1) / chunk;
+      arity = 2 * chunk;
+      prove_rand = 2 * chunk;
+      break;
+    default:
+      set_err("unknown kind %d", kind);
+      return PRIO3GPU_E_ARG;
+  }
+  g.bits = bits;
+  g.length = length;
+  g.chunk = (kind == PRIO3GPU_SUMVEC || kind == PRIO3GPU_HISTOGRAM) ? chunk : 0;
+  g.calls = calls;
+  g.arity = arity;
+  g.prove_rand_len = prove_rand;
+  g.m = next_pow2(1 + calls);
+  g.logm = ilog2(g.m);
+  if (g.m > 4096) {
+    set_err("gadget too large (m = %u)", g.m);
+    return PRIO3GPU_E_ARG;
+  }
+  g.gp_len = 2 * (g.m - 1) + 1;  // every gadget here has degree 2
+  g.proof_len = arity + g.gp_len;
+  g.verifier_len = 1 + arity + 1;
+  const uint32_t es = g.es;
+  g.leader_share_len = es * (g.meas_len + g.proof_len) + (g.jr_len ? 16 : 0);
+  g.helper_share_len = g.jr_len ? 48 : 32;
+  g.public_share_len = g.jr_len ? 32 : 0;
+  g.prep_share_len = es * g.verifier_len + (g.jr_len ? 16 : 0);
+  g.prep_msg_len = g.jr_len ? 16 : 0;
+
+  prio3gpu_sizes& s = c->sz;
+  s.field_size = es;
+  s.meas_len = g.meas_len;
+  s.proof_len = g.proof_len;
+  s.verifier_len = g.verifier_len;
+  s.joint_rand_len = g.jr_len;
+  s.output_len = g.out_len;
+  s.leader_input_share = g.leader_share_len;
+  s.helper_input_share = g.helper_share_len;
+  s.public_share = g.public_share_len;
+  s.prep_share = g.prep_share_len;
+  s.prep_msg = g.prep_msg_len;
+  s.aggregate_share = g.out_len * es;
+
+  // twiddles: alpha_m^k (k < m) and 1/m at index m, Montgomery form
+  const u128 p = (es == 16) ? P128 : P64;
+  const u128 R = (es == 16) ? (u128)0 - P128 /* 2^128 mod p */ : ((u128)1 << 64) % P64;
+  const u128 alpha = powmod(7, (p - 1) / g.m, p);
+  std::vector<uint8_t> tw((size_t)(g.m + 1) * es);
+  u128 a = 1;
+  for (uint32_t k = 0; k <= g.m; ++k) {
+    u128 v = (k < g.m) ? a : (p - (p - 1) / g.m);
+    u128 mv = mulmod(v, R, p);
+    for (uint32_t b = 0; b < es; ++b) tw[(size_t)k * es + b] = (uint8_t)(mv >> (8 * b));
+    a = mulmod(a, alpha, p);
+  }
+  CHK(c->twiddles.ensure(tw.size()));
+  HIPCHK(hipMemcpy(c->twiddles.p, tw.data(), tw.size(), hipMemcpyHostToDevice));
+  g.twiddles = c->twiddles.u8();
+  return 0;
+}
+
+// Make `src` (host or device, `bytes`) available on device; returns the device pointer.
+int stage_in(prio3gpu_ctx* c, DevBuf& buf, const void* src, size_t bytes, const uint8_t** out) {
+  if (!src || bytes == 0) {
+    *out = static_cast<const uint8_t*>(src);
+    return 0;
+  }
+  if (is_device_ptr(src)) {
+    *out = static_cast<const uint8_t*>(src);
+    return 0;
+  }
+  CHK(buf.ensure(bytes));
+  HIPCHK(hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+  *out = buf.u8();
+  return 0;
+}
+
+int copy_out(prio3gpu_ctx* c, void* dst, const void* dev_src, size_t bytes) {
+  if (!dst || bytes == 0 || dst == dev_src) return 0;
+  HIPCHK(hipMemcpyAsync(dst, dev_src, bytes, hipMemcpyDefault, c->stream));
+  return 0;
+}
+
+dim3 grid1(size_t n, uint32_t tpb) { return dim3((unsigned)((n + tpb - 1) / tpb)); }
+
+template <class FO>
+int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
+                        const uint8_t* d_pub, const uint8_t* d_in, uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  const uint32_t es = g.es;
+  const uint32_t N = (uint32_t)n;
+  const uint32_t TPB = 256;
+  uint64_t vk_lo, vk_hi;
+  memcpy(&vk_lo, c->vk, 8);
+  memcpy(&vk_hi, c->vk + 8, 8);
+  CRows nonces{d_nonces, 16};
+  CRows pub{d_pub, g.public_share_len};
+  Rows t_rows{st->t.u8(), 16};
+  hipLaunchKernelGGL(k_query_rand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N, vk_lo, vk_hi,
+                     nonces, t_rows, d_status);
+  CRows meas, proof, blinds;
+  if (st->agg_id == 0) {
+    meas = CRows{d_in, g.leader_share_len};
+    proof = CRows{d_in + (size_t)g.meas_len * es, g.leader_share_len};
+    blinds = CRows{d_in + (size_t)(g.meas_len + g.proof_len) * es, g.leader_share_len};
+  } else {
+    Rows mo{st->meas.u8(), (size_t)g.meas_len * es};
+    Rows po{st->proof.u8(), (size_t)g.proof_len * es};
+    hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
+                       (uint32_t)st->agg_id, CRows{d_in, g.helper_share_len}, mo, po, d_status);
+    meas = CRows{mo.base, mo.stride};
+    proof = CRows{po.base, po.stride};
+    blinds = CRows{d_in + 32, g.helper_share_len};
+  }
+  if (g.jr_len > 0) {
+    hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
+                       (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
+                       Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status);
+  }
+  // FLP query: block per report
+  FlpDims dims;
+  uint32_t nthr;
+  dims.rp_len = std::max(g.chunk, g.calls) + 1;
+  if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM) {
+    dims.cols = g.chunk;
+    if (g.chunk <= 256) {
+      dims.H = 256 / g.chunk;
+      if (dims.H > g.calls) dims.H = g.calls;
+      nthr = ((dims.H * g.chunk + 63) / 64) * 64;
+    } else {
+      dims.H = 1;
+      nthr = 256;
+    }
+  } else {
+    dims.cols = 1;
+    dims.H = 1;
+    nthr = (g.kind == KIND_SUM) ? 64 : 64;
+  }
+  const size_t esz = sizeof(typename FO::T);
+  size_t lds = esz * (6 * (size_t)g.m + dims.rp_len + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
+  lds = (lds + 15) & ~(size_t)15;
+  if (lds > 160 * 1024) {
+    set_err("FLP LDS requirement %zu too large", lds);
+    return PRIO3GPU_E_ARG;
+  }
+  hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr), lds, c->stream, g, N, dims, meas, proof,
+                     CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                     CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status);
+  HIPCHK(hipGetLastError());
+  st->meas_rows = meas;
+  st->n = n;
+  return 0;
+}
+
+template <class FO>
+int launch_decide(prio3gpu_ctx* c, size_t n, const uint8_t* d_l, const uint8_t* d_h,
+                  uint8_t* d_msg, uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  hipLaunchKernelGGL(k_decide<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
+                     CRows{d_l, g.prep_share_len}, CRows{d_h, g.prep_share_len},
+                     Rows{d_msg, g.prep_msg_len ? g.prep_msg_len : 16}, d_status);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// Segmented accumulation of the batch's output shares into agg slots.
+template <class FO>
+int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint32_t* slots,
+                      const uint8_t* d_status, prio3gpu_agg* agg) {
+  const Cfg& g = c->cfg;
+  // host-side grouping by slot (stable counting sort)
+  std::vector<uint32_t> hslots;
+  const uint32_t* sl = slots;
+  if (slots && is_device_ptr(slots)) {
+    hslots.resize(n);
+    HIPCHK(hipMemcpyAsync(hslots.data(), slots, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    sl = hslots.data();
+  }
+  const uint32_t S = agg->slots;
+  std::vector<uint32_t> cnt(S + 1, 0);
+  for (size_t r = 0; r < n; ++r) {
+    uint32_t s = sl ? sl[r] : 0;
+    if (s >= S) {
+      set_err("batch slot %u out of range (%u slots)", s, S);
+      return PRIO3GPU_E_ARG;
+    }
+    cnt[s + 1]++;
+  }
+  for (uint32_t s = 0; s < S; ++s) cnt[s + 1] += cnt[s];
+  auto& perm = c->h_perm;
+  perm.assign(n, 0);
+  {
+    std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
+    for (size_t r = 0; r < n; ++r) perm[pos[sl ? sl[r] : 0]++] = (uint32_t)r;
+  }
+  const uint32_t epb = std::min<uint32_t>(256, std::max<uint32_t>(1, g.out_len));
+  const uint32_t G = 256 / epb;
+  const uint32_t tiles = (g.out_len + epb - 1) / epb;
+  const size_t target_chunks = std::max<size_t>(1, 4096 / tiles);
+  size_t CH = std::max<size_t>(G, (n + target_chunks - 1) / target_chunks);
+  auto& cb = c->h_chunk_begin;
+  auto& cs = c->h_chunk_slot;
+  cb.clear();
+  cs.clear();
+  for (uint32_t s = 0; s < S; ++s) {
+    for (size_t b = cnt[s]; b < cnt[s + 1]; b += CH) {
+      cb.push_back((uint32_t)b);
+      cs.push_back(s);
+    }
+  }
+  const uint32_t nch = (uint32_t)cs.size();
+  if (nch == 0) return 0;
+  cb.push_back((uint32_t)n);
+  CHK(c->perm.ensure(n * 4));
+  CHK(c->chunks.ensure((size_t)(2 * nch + 1) * 4));
+  CHK(c->partials.ensure((size_t)nch * g.out_len * g.es));
+  CHK(c->pcounts.ensure((size_t)nch * 4));
+  HIPCHK(hipMemcpyAsync(c->perm.p, perm.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  uint32_t* d_cb = reinterpret_cast<uint32_t*>(c->chunks.p);
+  uint32_t* d_cs = d_cb + nch + 1;
+  HIPCHK(hipMemcpyAsync(d_cb, cb.data(), (nch + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d_cs, cs.data(), nch * 4, hipMemcpyHostToDevice, c->stream));
+  // The host vectors must outlive the async copies: synchronise before they can be reused.
+  hipLaunchKernelGGL(k_accum_partial<FO>, dim3(nch, tiles), dim3(256),
+                     256 * sizeof(typename FO::T), c->stream, g, st->meas_rows,
+                     reinterpret_cast<const uint32_t*>(c->perm.p), d_cb, d_status, epb,
+                     c->partials.u8(), reinterpret_cast<uint32_t*>(c->pcounts.p));
+  hipLaunchKernelGGL(k_accum_merge<FO>, grid1(g.out_len, 256), dim3(256), 0, c->stream, g, nch,
+                     d_cs, c->partials.u8(), reinterpret_cast<const uint32_t*>(c->pcounts.p),
+                     agg->share.u8(), reinterpret_cast<unsigned long long*>(agg->counts.p));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+template <class FO>
+int launch_out_shares(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_status,
+                      uint8_t* d_out) {
+  const Cfg& g = c->cfg;
+  dim3 grid((g.out_len + 255) / 256, (unsigned)n);
+  hipLaunchKernelGGL(k_out_shares<FO>, grid, dim3(256), 0, c->stream, g, (uint32_t)n,
+                     st->meas_rows, Rows{d_out, (size_t)g.out_len * g.es}, d_status);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+bool is_f64(const prio3gpu_ctx* c) { return c->cfg.es == 8; }
+
+int check_state(prio3gpu_ctx* c, prio3gpu_state* st, size_t n) {
+  if (!c || !st || st->ctx != c) {
+    set_err("bad context/state");
+    return PRIO3GPU_E_ARG;
+  }
+  if (n > st->cap) {
+    set_err("batch of %zu reports exceeds state capacity %zu", n, st->cap);
+    return PRIO3GPU_E_CAPACITY;
+  }
+  return 0;
+}
+
+// status: stage in (host or device) into st->status
+int stage_status(prio3gpu_ctx* c, DevBuf& buf, uint8_t* status, size_t n, uint8_t** d_status) {
+  if (!status) {
+    set_err("status array is required");
+    return PRIO3GPU_E_ARG;
+  }
+  if (is_device_ptr(status)) {
+    *d_status = status;
+    return 0;
+  }
+  CHK(buf.ensure(n));
+  HIPCHK(hipMemcpyAsync(buf.p, status, n, hipMemcpyHostToDevice, c->stream));
+  *d_status = buf.u8();
+  return 0;
+}
+
+}  // namespace
+
+// =================================================================================================
+// C ABI
+// =================================================================================================
+extern "C" {
+
+const char* prio3gpu_last_error(void) { return g_err.c_str(); }
+
+int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,
+                        const uint8_t verify_key[16], int device, prio3gpu_ctx** out) {
+  if (!out || !verify_key) {
+    set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  *out = nullptr;
+  HIPCHK(hipSetDevice(device));
+  auto* c = new prio3gpu_ctx();
+  c->device = device;
+  memcpy(c->vk, verify_key, 16);
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    set_err("hipStreamCreate: %s", hipGetErrorString(e));
+    delete c;
+    return PRIO3GPU_E_HIP;
+  }
+  int rc = setup_cfg(c, kind, bits, length, chunk_length);
+  if (rc) {
+    prio3gpu_ctx_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
+int prio3gpu_ctx_destroy(prio3gpu_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->twiddles.release();
+  for (auto& b : c->io) b.release();
+  c->perm.release();
+  c->chunks.release();
+  c->partials.release();
+  c->pcounts.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int prio3gpu_ctx_sizes(const prio3gpu_ctx* c, prio3gpu_sizes* out) {
+  if (!c || !out) {
+    set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  *out = c->sz;
+  return 0;
+}
+
+int prio3gpu_ctx_sync(prio3gpu_ctx* c) {
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+void* prio3gpu_ctx_stream(prio3gpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu_state** out) {
+  if (!c || !out || (agg_id != 0 && agg_id != 1) || capacity == 0) {
+    set_err("bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  auto* st = new prio3gpu_state();
+  st->ctx = c;
+  st->agg_id = agg_id;
+  st->cap = capacity;
+  const Cfg& g = c->cfg;
+  const size_t N = capacity;
+  int rc = 0;
+  rc |= st->t.ensure(N * 16);
+  rc |= st->jr.ensure(N * 16 * std::max<uint32_t>(1, g.jr_len));
+  rc |= st->part.ensure(N * 16);
+  rc |= st->seed.ensure(N * 16);
+  rc |= st->prep.ensure(N * g.prep_share_len);
+  rc |= st->msg.ensure(N * 16);
+  rc |= st->status.ensure(N);
+  if (agg_id == 1) {
+    rc |= st->meas.ensure(N * (size_t)g.meas_len * g.es);
+    rc |= st->proof.ensure(N * (size_t)g.proof_len * g.es);
+  }
+  if (rc) {
+    prio3gpu_state_destroy(st);
+    return PRIO3GPU_E_HIP;
+  }
+  *out = st;
+  return 0;
+}
+
+int prio3gpu_state_destroy(prio3gpu_state* st) {
+  if (!st) return 0;
+  if (st->ctx) (void)hipStreamSynchronize(st->ctx->stream);
+  for (DevBuf* b : {&st->t, &st->jr, &st->part, &st->seed, &st->meas, &st->proof, &st->prep,
+                    &st->msg, &st->status, &st->nonces, &st->pub, &st->input})
+    b->release();
+  delete st;
+  return 0;
+}
+
+int prio3gpu_agg_create(prio3gpu_ctx* c, uint32_t num_slots, prio3gpu_agg** out) {
+  if (!c || !out || num_slots == 0) {
+    set_err("bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  auto* a = new prio3gpu_agg();
+  a->ctx = c;
+  a->slots = num_slots;
+  if (a->share.ensure((size_t)num_slots * c->cfg.out_len * c->cfg.es) ||
+      a->counts.ensure((size_t)num_slots * 8)) {
+    prio3gpu_agg_destroy(a);
+    return PRIO3GPU_E_HIP;
+  }
+  *out = a;
+  return prio3gpu_agg_reset(a);
+}
+
+int prio3gpu_agg_destroy(prio3gpu_agg* a) {
+  if (!a) return 0;
+  a->share.release();
+  a->counts.release();
+  delete a;
+  return 0;
+}
+
+int prio3gpu_agg_reset(prio3gpu_agg* a) {
+  HIPCHK(hipMemsetAsync(a->share.p, 0, (size_t)a->slots * a->ctx->cfg.out_len * a->ctx->cfg.es,
+                        a->ctx->stream));
+  HIPCHK(hipMemsetAsync(a->counts.p, 0, (size_t)a->slots * 8, a->ctx->stream));
+  HIPCHK(hipStreamSynchronize(a->ctx->stream));
+  return 0;
+}
+
+int prio3gpu_agg_read(prio3gpu_agg* a, uint32_t slot, uint8_t* out_share, uint64_t* out_count) {
+  if (!a || slot >= a->slots) {
+    set_err("bad slot");
+    return PRIO3GPU_E_ARG;
+  }
+  prio3gpu_ctx* c = a->ctx;
+  const size_t bytes = (size_t)c->cfg.out_len * c->cfg.es;
+  if (out_share)
+    HIPCHK(hipMemcpyAsync(out_share, a->share.u8() + slot * bytes, bytes, hipMemcpyDefault,
+                          c->stream));
+  if (out_count)
+    HIPCHK(hipMemcpyAsync(out_count, a->counts.u8() + (size_t)slot * 8, 8, hipMemcpyDefault,
+                          c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_agg_merge_bytes(prio3gpu_agg* a, uint32_t slot, const uint8_t* share,
+                             uint64_t count) {
+  if (!a || slot >= a->slots || !share) {
+    set_err("bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  prio3gpu_ctx* c = a->ctx;
+  const size_t nel = c->cfg.out_len;
+  const size_t bytes = nel * c->cfg.es;
+  const uint8_t* d_src;
+  CHK(stage_in(c, c->io[0], share, bytes, &d_src));
+  uint8_t* dst = a->share.u8() + slot * bytes;
+  if (is_f64(c))
+    hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream, dst, d_src, nel);
+  else
+    hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream, dst, d_src, nel);
+  HIPCHK(hipGetLastError());
+  uint64_t cur = 0;
+  HIPCHK(hipMemcpyAsync(&cur, a->counts.u8() + (size_t)slot * 8, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  cur += count;
+  HIPCHK(hipMemcpyAsync(a->counts.u8() + (size_t)slot * 8, &cur, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* nonces,
+                          const uint8_t* public_shares, const uint8_t* input_shares,
+                          uint8_t* out_prep_shares, uint8_t* status) {
+  CHK(check_state(c, st, n));
+  if (n == 0) return 0;
+  if (!nonces || !input_shares || (c->cfg.jr_len && !public_shares)) {
+    set_err("null input");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const Cfg& g = c->cfg;
+  const uint8_t *d_nonces, *d_pub, *d_in;
+  CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));
+  CHK(stage_in(c, st->pub, public_shares, n * g.public_share_len, &d_pub));
+  const size_t in_len = st->agg_id == 0 ? g.leader_share_len : g.helper_share_len;
+  CHK(stage_in(c, st->input, input_shares, n * in_len, &d_in));
+  uint8_t* d_status;
+  CHK(stage_status(c, st->status, status, n, &d_status));
+  if (is_f64(c))
+    CHK(launch_prepare_init<Field64Ops>(c, st, n, d_nonces, d_pub, d_in, d_status));
+  else
+    CHK(launch_prepare_init<Field128Ops>(c, st, n, d_nonces, d_pub, d_in, d_status));
+  CHK(copy_out(c, out_prep_shares, st->prep.p, n * g.prep_share_len));
+  CHK(copy_out(c, status, d_status, n));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_prepare_shares_to_prepare_message(prio3gpu_ctx* c, size_t n,
+                                               const uint8_t* leader_prep_shares,
+                                               const uint8_t* helper_prep_shares,
+                                               uint8_t* out_prep_msgs, uint8_t* status) {
+  if (!c || !leader_prep_shares || !helper_prep_shares) {
+    set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  const Cfg& g = c->cfg;
+  const uint8_t *d_l, *d_h;
+  CHK(stage_in(c, c->io[0], leader_prep_shares, n * g.prep_share_len, &d_l));
+  CHK(stage_in(c, c->io[1], helper_prep_shares, n * g.prep_share_len, &d_h));
+  uint8_t* d_status;
+  CHK(stage_status(c, c->io[2], status, n, &d_status));
+  uint8_t* d_msg;
+  if (out_prep_msgs && is_device_ptr(out_prep_msgs)) {
+    d_msg = out_prep_msgs;
+  } else {
+    CHK(c->io[3].ensure(n * 16));
+    d_msg = c->io[3].u8();
+  }
+  if (is_f64(c))
+    CHK(launch_decide<Field64Ops>(c, n, d_l, d_h, d_msg, d_status));
+  else
+    CHK(launch_decide<Field128Ops>(c, n, d_l, d_h, d_msg, d_status));
+  CHK(copy_out(c, out_prep_msgs, d_msg, n * g.prep_msg_len));
+  CHK(copy_out(c, status, d_status, n));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_prepare_next(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* prep_msgs,
+                          uint8_t* status, uint8_t* out_output_shares, const uint32_t* batch_slots,
+                          prio3gpu_agg* agg) {
+  CHK(check_state(c, st, n));
+  if (n == 0) return 0;
+  if (n != st->n) {
+    set_err("prepare_next over %zu reports but %zu were prepared", n, st->n);
+    return PRIO3GPU_E_ARG;
+  }
+  if (agg && agg->ctx != c) {
+    set_err("aggregate belongs to another context");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const Cfg& g = c->cfg;
+  uint8_t* d_status;
+  CHK(stage_status(c, st->status, status, n, &d_status));
+  if (g.jr_len) {
+    if (!prep_msgs) {
+      set_err("prep messages required");
+      return PRIO3GPU_E_ARG;
+    }
+    const uint8_t* d_msgs;
+    CHK(stage_in(c, c->io[4], prep_msgs, n * 16, &d_msgs));
+    hipLaunchKernelGGL(k_prepare_next, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
+                       CRows{d_msgs, 16}, CRows{st->seed.u8(), 16}, d_status);
+    HIPCHK(hipGetLastError());
+  }
+  if (out_output_shares) {
+    const size_t bytes = n * (size_t)g.out_len * g.es;
+    uint8_t* d_out;
+    if (is_device_ptr(out_output_shares)) {
+      d_out = out_output_shares;
+    } else {
+      CHK(c->io[5].ensure(bytes));
+      d_out = c->io[5].u8();
+    }
+    if (is_f64(c))
+      CHK(launch_out_shares<Field64Ops>(c, st, n, d_status, d_out));
+    else
+      CHK(launch_out_shares<Field128Ops>(c, st, n, d_status, d_out));
+    CHK(copy_out(c, out_output_shares, d_out, bytes));
+  }
+  if (agg) {
+    if (is_f64(c))
+      CHK(launch_accumulate<Field64Ops>(c, st, n, batch_slots, d_status, agg));
+    else
+      CHK(launch_accumulate<Field128Ops>(c, st, n, batch_slots, d_status, agg));
+  }
+  CHK(copy_out(c, status, d_status, n));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_helper_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* nonces,
+                         const uint8_t* public_shares, const uint8_t* helper_input_shares,
+                         const uint8_t* leader_prep_shares, const uint32_t* batch_slots,
+                         uint8_t* out_prep_msgs, uint8_t* status, prio3gpu_agg* agg) {
+  CHK(check_state(c, st, n));
+  if (st->agg_id != 1) {
+    set_err("helper_init needs a helper (agg_id 1) state");
+    return PRIO3GPU_E_ARG;
+  }
+  if (n == 0) return 0;
+  if (!nonces || !helper_input_shares || !leader_prep_shares || (c->cfg.jr_len && !public_shares)) {
+    set_err("null input");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const Cfg& g = c->cfg;
+  const uint8_t *d_nonces, *d_pub, *d_in, *d_lps;
+  CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));
+  CHK(stage_in(c, st->pub, public_shares, n * g.public_share_len, &d_pub));
+  CHK(stage_in(c, st->input, helper_input_shares, n * g.helper_share_len, &d_in));
+  CHK(stage_in(c, c->io[0], leader_prep_shares, n * g.prep_share_len, &d_lps));
+  uint8_t* d_status;
+  CHK(stage_status(c, st->status, status, n, &d_status));
+  const bool f64 = is_f64(c);
+  if (f64)
+    CHK(launch_prepare_init<Field64Ops>(c, st, n, d_nonces, d_pub, d_in, d_status));
+  else
+    CHK(launch_prepare_init<Field128Ops>(c, st, n, d_nonces, d_pub, d_in, d_status));
+  uint8_t* d_msg = st->msg.u8();
+  if (f64)
+    CHK(launch_decide<Field64Ops>(c, n, d_lps, st->prep.u8(), d_msg, d_status));
+  else
+    CHK(launch_decide<Field128Ops>(c, n, d_lps, st->prep.u8(), d_msg, d_status));
+  if (g.jr_len) {
+    hipLaunchKernelGGL(k_prepare_next, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
+                       CRows{d_msg, 16}, CRows{st->seed.u8(), 16}, d_status);
+    HIPCHK(hipGetLastError());
+  }
+  if (agg) {
+    if (f64)
+      CHK(launch_accumulate<Field64Ops>(c, st, n, batch_slots, d_status, agg));
+    else
+      CHK(launch_accumulate<Field128Ops>(c, st, n, batch_slots, d_status, agg));
+  }
+  CHK(copy_out(c, out_prep_msgs, d_msg, n * g.prep_msg_len));
+  CHK(copy_out(c, status, d_status, n));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_comm_unique_id(uint8_t out_id[128]) {
+  ncclUniqueId id;
+  RCCLCHK(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "unique id size");
+  memcpy(out_id, &id, 128);
+  return 0;
+}
+
+int prio3gpu_comm_init(const uint8_t id[128], int nranks, int rank, int device,
+                       prio3gpu_comm** out) {
+  HIPCHK(hipSetDevice(device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, 128);
+  auto* cm = new prio3gpu_comm();
+  cm->nranks = nranks;
+  cm->rank = rank;
+  cm->device = device;
+  ncclResult_t e = ncclCommInitRank(&cm->comm, nranks, uid, rank);
+  if (e != ncclSuccess) {
+    set_err("ncclCommInitRank: %s", ncclGetErrorString(e));
+    delete cm;
+    return PRIO3GPU_E_RCCL;
+  }
+  *out = cm;
+  return 0;
+}
+
+int prio3gpu_comm_destroy(prio3gpu_comm* cm) {
+  if (!cm) return 0;
+  cm->gather.release();
+  cm->cgather.release();
+  if (cm->comm) ncclCommDestroy(cm->comm);
+  delete cm;
+  return 0;
+}
+
+int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* a) {
+  if (!cm || !c || !a || a->ctx != c) {
+    set_err("bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const size_t nel = (size_t)a->slots * c->cfg.out_len;
+  const size_t bytes = nel * c->cfg.es;
+  CHK(cm->gather.ensure(bytes * cm->nranks));
+  // all-gather raw LE field-element bytes, then sum every rank's share (rank order) mod p
+  RCCLCHK(ncclAllGather(a->share.p, cm->gather.p, bytes, ncclUint8, cm->comm, c->stream));
+  RCCLCHK(ncclAllReduce(a->counts.p, a->counts.p, a->slots, ncclUint64, ncclSum, cm->comm,
+                        c->stream));
+  HIPCHK(hipMemsetAsync(a->share.p, 0, bytes, c->stream));
+  for (int r = 0; r < cm->nranks; ++r) {
+    const uint8_t* src = cm->gather.u8() + (size_t)r * bytes;
+    if (is_f64(c))
+      hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
+                         a->share.u8(), src, nel);
+    else
+      hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
+                         a->share.u8(), src, nel);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_dev_alloc(prio3gpu_ctx* c, size_t bytes, void** out) {
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMalloc(out, bytes ? bytes : 16));
+  return 0;
+}
+int prio3gpu_dev_free(prio3gpu_ctx* c, void* p) {
+  (void)c;
+  HIPCHK(hipFree(p));
+  return 0;
+}
+int prio3gpu_memcpy(prio3gpu_ctx* c, void* dst, const void* src, size_t bytes) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,224 @@
+// Field64 / Field128 arithmetic for gfx950 (CDNA4), 32-bit-limb Montgomery built from
+// v_mad_u64_u32 chains.  Replaces prio 0.15.1 `src/fp.rs` / `src/field.rs` (ext crate, called from
+// the Prio3 prepare path at aggregator/src/aggregator.rs:1777-1786).
+//
+// Values are stored CANONICALLY (the DAP little-endian encoding is the storage format).  Constants
+// derived inside kernels (roots of unity, powers of t / r, Lagrange weights) are kept in Montgomery
+// form (x*R), so   mul(mont_const, canonical) == canonical product   and no conversions are needed
+// on the data path.
+//
+//   Field64 : p = 2^64 - 2^32 + 1,        R = 2^64,  -p^-1 mod 2^32 = 0xFFFFFFFF
+//   Field128: p = 2^128 - 28*2^64 + 1,    R = 2^128, -p^-1 mod 2^32 = 0xFFFFFFFF
+// Both primes are == 1 mod 2^32, so each CIOS reduction word is m = -t0 and the m*p[0] product
+// vanishes; the zero limbs of p fold away at compile time.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DEVI __device__ __forceinline__
+
+struct F128 {
+  uint32_t w[4];
+};
+struct F64 {
+  uint32_t w[2];
+};
+
+// ----------------------------------------------------------------------------------------------
+// Field128
+// ----------------------------------------------------------------------------------------------
+struct Field128Ops {
+  using T = F128;
+  static constexpr int ES = 16;      // encoded size
+  static constexpr int NW = 4;       // 32-bit limbs
+  static constexpr uint32_t P0 = 1u, P1 = 0u, P2 = 0xFFFFFFE4u, P3 = 0xFFFFFFFFu;
+
+  static DEVI F128 zero() { return F128{{0u, 0u, 0u, 0u}}; }
+  // R mod p = 2^128 - p = 28*2^64 - 1  (Montgomery form of 1)
+  static DEVI F128 one_mont() { return F128{{0xFFFFFFFFu, 0xFFFFFFFFu, 0x1Bu, 0u}}; }
+  // R^2 mod p = 0x5587fffffffffffffcf1
+  static DEVI F128 r2() { return F128{{0xFFFFFCF1u, 0xFFFFFFFFu, 0x5587u, 0u}}; }
+  static DEVI F128 one() { return F128{{1u, 0u, 0u, 0u}}; }
+  // (p+1)/2, canonical  (1/2)
+  static DEVI F128 half() { return F128{{1u, 0u, 0xFFFFFFF2u, 0x7FFFFFFFu}}; }
+
+  static DEVI bool is_canonical(const F128& a) {
+    // a < p  <=>  !(a >= p).  p = [1, 0, P2, P3]
+    if (a.w[3] != P3) return a.w[3] < P3;
+    if (a.w[2] != P2) return a.w[2] < P2;
+    if (a.w[1] != 0u) return false;
+    return a.w[0] < 1u;
+  }
+  static DEVI bool eq(const F128& a, const F128& b) {
+    return ((a.w[0] ^ b.w[0]) | (a.w[1] ^ b.w[1]) | (a.w[2] ^ b.w[2]) | (a.w[3] ^ b.w[3])) == 0u;
+  }
+  static DEVI bool is_zero(const F128& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3]) == 0u; }
+
+  // a + b mod p.  With c = 2^128 - p = [FFFFFFFF, FFFFFFFF, 1B, 0]:
+  //   s = a + b (carry k1);  u = s + c (carry k2);  result = (k1|k2) ? u : s.
+  static DEVI F128 add(const F128& a, const F128& b) {
+    uint64_t t;
+    uint32_t s0, s1, s2, s3, k1;
+    t = (uint64_t)a.w[0] + b.w[0];            s0 = (uint32_t)t;
+    t = (uint64_t)a.w[1] + b.w[1] + (t >> 32); s1 = (uint32_t)t;
+    t = (uint64_t)a.w[2] + b.w[2] + (t >> 32); s2 = (uint32_t)t;
+    t = (uint64_t)a.w[3] + b.w[3] + (t >> 32); s3 = (uint32_t)t; k1 = (uint32_t)(t >> 32);
+    uint32_t u0, u1, u2, u3, k2;
+    t = (uint64_t)s0 + 0xFFFFFFFFu;            u0 = (uint32_t)t;
+    t = (uint64_t)s1 + 0xFFFFFFFFu + (t >> 32); u1 = (uint32_t)t;
+    t = (uint64_t)s2 + 0x1Bu + (t >> 32);       u2 = (uint32_t)t;
+    t = (uint64_t)s3 + (t >> 32);               u3 = (uint32_t)t; k2 = (uint32_t)(t >> 32);
+    bool sel = (k1 | k2) != 0u;
+    return F128{{sel ? u0 : s0, sel ? u1 : s1, sel ? u2 : s2, sel ? u3 : s3}};
+  }
+  // a - b mod p: d = a - b (borrow) ; if borrow: d += p
+  static DEVI F128 sub(const F128& a, const F128& b) {
+    int64_t t;
+    uint32_t d0, d1, d2, d3;
+    uint64_t u;
+    u = (uint64_t)a.w[0] - b.w[0];                        d0 = (uint32_t)u; t = (int64_t)u >> 32;
+    u = (uint64_t)a.w[1] - b.w[1] + (uint64_t)t;          d1 = (uint32_t)u; t = (int64_t)u >> 32;
+    u = (uint64_t)a.w[2] - b.w[2] + (uint64_t)t;          d2 = (uint32_t)u; t = (int64_t)u >> 32;
+    u = (uint64_t)a.w[3] - b.w[3] + (uint64_t)t;          d3 = (uint32_t)u; t = (int64_t)u >> 32;
+    uint32_t m = (uint32_t)t;  // 0 or 0xFFFFFFFF
+    // add p & m
+    uint64_t c;
+    c = (uint64_t)d0 + (P0 & m);            d0 = (uint32_t)c;
+    c = (uint64_t)d1 + (P1 & m) + (c >> 32); d1 = (uint32_t)c;
+    c = (uint64_t)d2 + (P2 & m) + (c >> 32); d2 = (uint32_t)c;
+    c = (uint64_t)d3 + (P3 & m) + (c >> 32); d3 = (uint32_t)c;
+    return F128{{d0, d1, d2, d3}};
+  }
+  static DEVI F128 neg(const F128& a) { return sub(zero(), a); }
+  static DEVI F128 dbl(const F128& a) { return add(a, a); }
+
+  // Montgomery product a*b*2^-128 mod p (CIOS, 32-bit words).  Inputs < p, output < p.
+  static DEVI F128 mul(const F128& a, const F128& b) {
+    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t bi = b.w[i];
+      uint64_t c;
+      c = (uint64_t)a.w[0] * bi + t0;              t0 = (uint32_t)c;
+      c = (uint64_t)a.w[1] * bi + t1 + (c >> 32);  t1 = (uint32_t)c;
+      c = (uint64_t)a.w[2] * bi + t2 + (c >> 32);  t2 = (uint32_t)c;
+      c = (uint64_t)a.w[3] * bi + t3 + (c >> 32);  t3 = (uint32_t)c;
+      c = (uint64_t)t4 + (c >> 32);
+      t4 = (uint32_t)c;
+      uint32_t t5 = (uint32_t)(c >> 32);
+      // reduction word m = -t0 ; t0 + m*P0 = t0 + m == 0 mod 2^32 with carry (t0 != 0)
+      const uint32_t m = 0u - t0;
+      c = (uint64_t)t1 + (t0 != 0u ? 1u : 0u);     t0 = (uint32_t)c;  // + m*P1 (=0)
+      c = (uint64_t)m * P2 + t2 + (c >> 32);       t1 = (uint32_t)c;
+      c = (uint64_t)m * P3 + t3 + (c >> 32);       t2 = (uint32_t)c;
+      c = (uint64_t)t4 + (c >> 32);                t3 = (uint32_t)c;
+      t4 = t5 + (uint32_t)(c >> 32);
+    }
+    // t < 2p: conditional subtract
+    F128 r{{t0, t1, t2, t3}};
+    if (t4 != 0u || !is_canonical(r)) {
+      // r - p mod 2^128  ==  r + c  mod 2^128
+      uint64_t c;
+      c = (uint64_t)t0 + 0xFFFFFFFFu;            r.w[0] = (uint32_t)c;
+      c = (uint64_t)t1 + 0xFFFFFFFFu + (c >> 32); r.w[1] = (uint32_t)c;
+      c = (uint64_t)t2 + 0x1Bu + (c >> 32);       r.w[2] = (uint32_t)c;
+      c = (uint64_t)t3 + (c >> 32);               r.w[3] = (uint32_t)c;
+    }
+    return r;
+  }
+  static DEVI F128 to_mont(const F128& a) { return mul(a, r2()); }
+  static DEVI F128 from_mont(const F128& a) { return mul(a, one()); }
+
+  static DEVI F128 load(const uint8_t* p) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    return F128{{v.x, v.y, v.z, v.w}};
+  }
+  static DEVI void store(uint8_t* p, const F128& a) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(a.w[0], a.w[1], a.w[2], a.w[3]);
+  }
+  static DEVI F128 from_u64x2(uint64_t lo, uint64_t hi) {
+    return F128{{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)}};
+  }
+  static DEVI F128 from_u32(uint32_t x) { return F128{{x, 0u, 0u, 0u}}; }
+};
+
+// ----------------------------------------------------------------------------------------------
+// Field64 (Goldilocks).  Used by Prio3Count only.
+// ----------------------------------------------------------------------------------------------
+struct Field64Ops {
+  using T = F64;
+  static constexpr int ES = 8;
+  static constexpr int NW = 2;
+  static constexpr uint32_t P0 = 1u, P1 = 0xFFFFFFFFu;
+
+  static DEVI F64 zero() { return F64{{0u, 0u}}; }
+  static DEVI F64 one_mont() { return F64{{0xFFFFFFFFu, 0u}}; }          // 2^64 mod p
+  static DEVI F64 r2() { return F64{{0x00000001u, 0xFFFFFFFEu}}; }       // 2^128 mod p
+  static DEVI F64 one() { return F64{{1u, 0u}}; }
+  static DEVI F64 half() { return F64{{0x80000001u, 0x7FFFFFFFu}}; }      // (p+1)/2
+
+  static DEVI uint64_t u(const F64& a) { return ((uint64_t)a.w[1] << 32) | a.w[0]; }
+  static DEVI F64 mk(uint64_t x) { return F64{{(uint32_t)x, (uint32_t)(x >> 32)}}; }
+  static constexpr uint64_t P = 0xFFFFFFFF00000001ull;
+
+  static DEVI bool is_canonical(const F64& a) { return u(a) < P; }
+  static DEVI bool eq(const F64& a, const F64& b) { return u(a) == u(b); }
+  static DEVI bool is_zero(const F64& a) { return u(a) == 0ull; }
+  static DEVI F64 add(const F64& a, const F64& b) {
+    uint64_t x = u(a), y = u(b);
+    uint64_t s = x + y;
+    bool carry = s < x;
+    uint64_t t = s + 0xFFFFFFFFull;  // s - p mod 2^64
+    bool carry2 = t < s;
+    return mk((carry || carry2) ? t : s);
+  }
+  static DEVI F64 sub(const F64& a, const F64& b) {
+    uint64_t x = u(a), y = u(b);
+    uint64_t d = x - y;
+    return mk(x < y ? d + P : d);
+  }
+  static DEVI F64 neg(const F64& a) { return sub(zero(), a); }
+  static DEVI F64 dbl(const F64& a) { return add(a, a); }
+  static DEVI F64 mul(const F64& a, const F64& b) {
+    uint32_t t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t bi = b.w[i];
+      uint64_t c;
+      c = (uint64_t)a.w[0] * bi + t0;             t0 = (uint32_t)c;
+      c = (uint64_t)a.w[1] * bi + t1 + (c >> 32); t1 = (uint32_t)c;
+      c = (uint64_t)t2 + (c >> 32);
+      t2 = (uint32_t)c;
+      uint32_t t3 = (uint32_t)(c >> 32);
+      const uint32_t m = 0u - t0;
+      c = (uint64_t)m * P1 + t1 + (t0 != 0u ? 1u : 0u); t0 = (uint32_t)c;
+      c = (uint64_t)t2 + (c >> 32);                     t1 = (uint32_t)c;
+      t2 = t3 + (uint32_t)(c >> 32);
+    }
+    uint64_t r = ((uint64_t)t1 << 32) | t0;
+    if (t2 != 0u || r >= P) r = r + 0xFFFFFFFFull;  // r - p mod 2^64
+    return mk(r);
+  }
+  static DEVI F64 to_mont(const F64& a) { return mul(a, r2()); }
+  static DEVI F64 from_mont(const F64& a) { return mul(a, one()); }
+  static DEVI F64 load(const uint8_t* p) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    return F64{{v.x, v.y}};
+  }
+  static DEVI void store(uint8_t* p, const F64& a) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(a.w[0], a.w[1]);
+  }
+  static DEVI F64 from_u32(uint32_t x) { return F64{{x, 0u}}; }
+};
+
+// Montgomery-form power x^e (x in Montgomery form, result Montgomery form).
+template <class FO>
+DEVI typename FO::T mont_pow(typename FO::T x, uint64_t e) {
+  typename FO::T r = FO::one_mont();
+  while (e) {
+    if (e & 1) r = FO::mul(r, x);
+    x = FO::mul(x, x);
+    e >>= 1;
+  }
+  return r;
+}

@@ -1,0 +1,740 @@
+// Batched Prio3 preparation kernels for gfx950 (MI355X).
+//
+// The reference runs Prio3 one report at a time inside prio 0.15.1 (ext crate) from
+//   helper:  aggregator/src/aggregator.rs:1613-1848  (helper_initialized + evaluate, :1775-1797)
+//   leader:  aggregator/src/aggregator/aggregation_job_driver.rs:329-402 (:362-380) and
+//            :566-686 (leader_continued, :579-593)
+//   accumulate: aggregator/src/aggregator/accumulator.rs:76-122
+// Here a whole aggregation job (or several) is one batch, processed by these kernels:
+//
+//   k_query_rand   lane/report  XOF(verify_key, dst5, nonce) -> t                     (1 perm)
+//   k_expand       lane/report  helper: XOF(seed, dst1|dst2, [1]) -> meas/proof share (MEAS/10.5 perms)
+//   k_jr           lane/report  joint-rand part over the encoded meas share, corrected seed,
+//                               joint randomness                                      (MEAS/10.5 perms)
+//   k_flp_query    block/report FLP query: circuit output, wire polys at t (Lagrange weights from
+//                               one size-m NTT, no inversions), gadget poly at alpha^k (NTT) and t
+//   k_decide       lane/report  sum verifier shares, decide, prep msg (1 perm)
+//   k_prepare_next lane/report  prep msg == corrected seed
+//   k_accum_*      segmented modular sum of truncated output shares into per-batch aggregates
+//   k_merge        aggregate += other aggregate (mod p) after the RCCL all-gather
+#pragma once
+#include "field.h"
+#include "keccak.h"
+
+namespace p3g {
+
+enum Kind : uint32_t { KIND_COUNT = 0, KIND_SUM = 1, KIND_SUMVEC = 2, KIND_HISTOGRAM = 3 };
+
+// Per-report status codes = DAP PrepareError (messages/src/lib.rs:2288-2298) + 0 = ok.
+enum Status : uint8_t { ST_OK = 0, ST_VDAF_PREP_ERROR = 5, ST_INVALID_MESSAGE = 8, ST_SKIPPED = 0xFF };
+
+enum Usage : uint32_t {
+  DST_MEASUREMENT_SHARE = 1,
+  DST_PROOF_SHARE = 2,
+  DST_JOINT_RANDOMNESS = 3,
+  DST_PROVE_RANDOMNESS = 4,
+  DST_QUERY_RANDOMNESS = 5,
+  DST_JOINT_RAND_SEED = 6,
+  DST_JOINT_RAND_PART = 7,
+};
+
+struct Cfg {
+  uint32_t kind, algo_id, es;
+  uint32_t meas_len, proof_len, verifier_len, jr_len, out_len, prove_rand_len;
+  uint32_t bits, length, chunk, calls, m, logm, arity, gp_len;
+  uint32_t leader_share_len, helper_share_len, public_share_len, prep_share_len, prep_msg_len;
+  const uint8_t* twiddles;  // device: alpha_m^k, k < m, Montgomery form, ES bytes each
+};
+
+// A per-report byte array: element r at base + r*stride.
+struct Rows {
+  uint8_t* base;
+  size_t stride;
+  DEVI uint8_t* at(size_t r) const { return base + r * stride; }
+};
+struct CRows {
+  const uint8_t* base;
+  size_t stride;
+  DEVI const uint8_t* at(size_t r) const { return base + r * stride; }
+};
+
+DEVI uint64_t ld64(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
+DEVI void st64(uint8_t* p, uint64_t v) { *reinterpret_cast<uint64_t*>(p) = v; }
+
+// ------------------------------------------------------------------------------------------------
+// Squeeze n field elements (prio `into_field_vec`: ES-byte LE chunks, reject >= p) from a state
+// that has just been permuted after absorbing.  Accepted element i goes to out + i*ES.
+// ------------------------------------------------------------------------------------------------
+template <class FO, int NR>
+DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out);
+
+template <>
+DEVI void squeeze_vec<Field128Ops, 24>(uint64_t s[25], uint32_t n, uint8_t* out) {
+  using FO = Field128Ops;
+  uint32_t cnt = 0;
+  while (true) {
+    // block A: elements (s0,s1)..(s18,s19); s20 = low half of the element straddling blocks
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
+      if (cnt < n && FO::is_canonical(e)) {
+        FO::store(out + (size_t)cnt * 16, e);
+        ++cnt;
+      }
+    }
+    if (cnt >= n) break;
+    const uint64_t carry = s[20];
+    keccak_p<24>(s);
+    {
+      F128 e = FO::from_u64x2(carry, s[0]);
+      if (cnt < n && FO::is_canonical(e)) {
+        FO::store(out + (size_t)cnt * 16, e);
+        ++cnt;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
+      if (cnt < n && FO::is_canonical(e)) {
+        FO::store(out + (size_t)cnt * 16, e);
+        ++cnt;
+      }
+    }
+    if (cnt >= n) break;
+    keccak_p<24>(s);
+  }
+}
+
+template <>
+DEVI void squeeze_vec<Field64Ops, 24>(uint64_t s[25], uint32_t n, uint8_t* out) {
+  using FO = Field64Ops;
+  uint32_t cnt = 0;
+  while (true) {
+#pragma unroll
+    for (int k = 0; k < 21; ++k) {
+      if (cnt < n && s[k] < FO::P) {
+        st64(out + (size_t)cnt * 8, s[k]);
+        ++cnt;
+      }
+    }
+    if (cnt >= n) break;
+    keccak_p<24>(s);
+  }
+}
+
+// XOF(seed, dst(usage), binder=[byte]) expanded into n elements (helper share expansion).
+template <class FO>
+DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed_lo,
+                                 uint64_t seed_hi, uint32_t binder_byte, uint32_t n,
+                                 uint8_t* out) {
+  MsgBlock m;
+  m.clear();
+  m.header(algo_id, usage, seed_lo, seed_hi);
+  m.put8(25, binder_byte);
+  m.pad(26);
+  uint64_t s[25];
+  sponge_one_block<24>(s, m);
+  squeeze_vec<FO, 24>(s, n, out);
+}
+
+// derive_seed(0^16, dst6, part0 || part1)   (prio Prio3::derive_joint_rand_seed)
+DEVI void derive_jr_seed(uint32_t algo_id, uint64_t p0lo, uint64_t p0hi, uint64_t p1lo,
+                         uint64_t p1hi, uint64_t& olo, uint64_t& ohi) {
+  MsgBlock m;
+  m.clear();
+  m.header(algo_id, DST_JOINT_RAND_SEED, 0ull, 0ull);
+  m.put64(25, p0lo);
+  m.put64(33, p0hi);
+  m.put64(41, p1lo);
+  m.put64(49, p1hi);
+  m.pad(57);
+  uint64_t s[25];
+  sponge_one_block<24>(s, m);
+  olo = s[0];
+  ohi = s[1];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Joint-randomness part (prio prepare_init / shard):
+//   derive_seed(blind, dst7, [agg_id] || nonce || encode(meas_share))
+// Message = 42-byte prefix || data (nbytes, multiple of 8) || SHAKE padding.  Stream word g >= 5 is
+// (D[g-6] >> 48) | (D[g-5] << 16) with D[-1] = the top 16 bits of the nonce's high word.
+// ------------------------------------------------------------------------------------------------
+// word g >= 5 of the stream:  (D[i-1] >> 48) | (D[i] << 16),  i = g - 5,  D[-1] = nonce_hi
+DEVI uint64_t jr_data_word(int64_t g, const uint8_t* data, int64_t nd, uint64_t nonce_hi) {
+  const int64_t i = g - 5;
+  uint64_t lo = (i == 0) ? (nonce_hi >> 48) : ((i - 1 < nd) ? (ld64(data + 8 * (i - 1)) >> 48) : 0ull);
+  uint64_t hi = (i < nd) ? (ld64(data + 8 * i) << 16) : 0ull;
+  return lo | hi;
+}
+
+DEVI void jr_part(uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t blind_hi,
+                  uint64_t nonce_lo, uint64_t nonce_hi, const uint8_t* data, uint32_t nbytes,
+                  uint64_t& olo, uint64_t& ohi) {
+  MsgBlock pre;
+  pre.clear();
+  pre.header(algo_id, DST_JOINT_RAND_PART, blind_lo, blind_hi);
+  pre.put8(25, agg_id);
+  pre.put64(26, nonce_lo);
+  pre.put64(34, nonce_hi);
+  // bytes 40,41 (top of nonce_hi) live in word 5 together with data; words 0..4 are pure prefix
+  const int64_t nd = nbytes / 8;
+  const int64_t total = 42 + (int64_t)nbytes;   // message bytes before padding
+  const int64_t nblocks = total / 168 + 1;
+  const int64_t padw = total >> 3;              // word holding the 0x1F pad byte
+  const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
+  uint64_t s[25];
+  // block 0 (prefix + first data words)
+#pragma unroll
+  for (int w = 0; w < 21; ++w) {
+    uint64_t v = (w < 5) ? pre.w[w] : jr_data_word(w, data, nd, nonce_hi);
+    if (padw == w) v ^= padv;
+    if (nblocks == 1 && w == 20) v ^= 0x8000000000000000ull;
+    s[w] = v;
+  }
+#pragma unroll
+  for (int i = 21; i < 25; ++i) s[i] = 0ull;
+  keccak_p<24>(s);
+  for (int64_t b = 1; b < nblocks; ++b) {
+    // fast path: every word of the block is data:  D index 21b+20-5 < nd  and no padding inside
+    const bool fast = (21 * b + 15 < nd) && (21 * b + 20 < padw);
+    if (fast) {
+      const uint64_t* D = reinterpret_cast<const uint64_t*>(data) + (21 * b - 6);
+      uint64_t prev = D[0];
+#pragma unroll
+      for (int w = 0; w < 21; ++w) {
+        const uint64_t cur = D[w + 1];
+        s[w] ^= (prev >> 48) | (cur << 16);
+        prev = cur;
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 21; ++w) {
+        const int64_t g = 21 * b + w;
+        uint64_t v = jr_data_word(g, data, nd, nonce_hi);
+        if (padw == g) v ^= padv;
+        if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
+        s[w] ^= v;
+      }
+    }
+    keccak_p<24>(s);
+  }
+  olo = s[0];
+  ohi = s[1];
+}
+
+// ================================================================================================
+// Kernels
+// ================================================================================================
+
+// t = XOF(verify_key, dst5, nonce).next_vec(1)    (prio prepare_init, query randomness)
+template <class FO>
+__global__ void __launch_bounds__(256) k_query_rand(Cfg cfg, uint32_t n, uint64_t vk_lo,
+                                                    uint64_t vk_hi, CRows nonces, Rows out_t,
+                                                    const uint8_t* status) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (status && status[r] != ST_OK) return;
+  const uint8_t* nz = nonces.at(r);
+  MsgBlock m;
+  m.clear();
+  m.header(cfg.algo_id, DST_QUERY_RANDOMNESS, vk_lo, vk_hi);
+  m.put64(25, ld64(nz));
+  m.put64(33, ld64(nz + 8));
+  m.pad(41);
+  uint64_t s[25];
+  sponge_one_block<24>(s, m);
+  squeeze_vec<FO, 24>(s, 1, out_t.at(r));
+}
+
+// Helper share expansion: meas share XOF(k_meas, dst1, [agg_id]) and proof share
+// XOF(k_proof, dst2, [agg_id]) (prio prepare_init, Share::Helper arms).
+template <class FO>
+__global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t agg_id,
+                                                CRows helper_shares, Rows out_meas,
+                                                Rows out_proof, const uint8_t* status) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (status && status[r] != ST_OK) return;
+  const uint8_t* hs = helper_shares.at(r);
+  xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), agg_id,
+                             cfg.proof_len, out_proof.at(r));
+  xof_expand_byte_binder<FO>(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8), agg_id,
+                             cfg.meas_len, out_meas.at(r));
+}
+
+// Joint randomness (prio prepare_init): own part over the encoded meas share, corrected seed
+// (public-share parts with this aggregator's part replaced), joint_rand = XOF(seed, dst3, "").
+template <class FO>
+__global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id, CRows nonces,
+                                            CRows public_shares, CRows blinds, CRows meas,
+                                            Rows out_part, Rows out_seed, Rows out_jr,
+                                            const uint8_t* status) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (status && status[r] != ST_OK) return;
+  const uint8_t* nz = nonces.at(r);
+  const uint8_t* bl = blinds.at(r);
+  uint64_t plo, phi;
+  jr_part(cfg.algo_id, agg_id, ld64(bl), ld64(bl + 8), ld64(nz), ld64(nz + 8), meas.at(r),
+          cfg.meas_len * cfg.es, plo, phi);
+  st64(out_part.at(r), plo);
+  st64(out_part.at(r) + 8, phi);
+  const uint8_t* ps = public_shares.at(r);
+  uint64_t p0lo = ld64(ps), p0hi = ld64(ps + 8), p1lo = ld64(ps + 16), p1hi = ld64(ps + 24);
+  if (agg_id == 0) {
+    p0lo = plo;
+    p0hi = phi;
+  } else {
+    p1lo = plo;
+    p1hi = phi;
+  }
+  uint64_t slo, shi;
+  derive_jr_seed(cfg.algo_id, p0lo, p0hi, p1lo, p1hi, slo, shi);
+  st64(out_seed.at(r), slo);
+  st64(out_seed.at(r) + 8, shi);
+  MsgBlock m;
+  m.clear();
+  m.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
+  m.pad(25);
+  uint64_t s[25];
+  sponge_one_block<24>(s, m);
+  squeeze_vec<FO, 24>(s, cfg.jr_len, out_jr.at(r));
+}
+
+// ------------------------------------------------------------------------------------------------
+// LDS helpers
+// ------------------------------------------------------------------------------------------------
+DEVI uint32_t bitrev(uint32_t x, uint32_t logn) {
+  return logn == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - logn));
+}
+
+template <class FO>
+DEVI typename FO::T ld_tw(const Cfg& cfg, uint32_t i) {
+  return FO::load(cfg.twiddles + (size_t)i * FO::ES);
+}
+
+// Two in-place radix-2 DIT NTTs of size m (inputs already bit-reversed) over LDS arrays A and B,
+// twiddles in Montgomery form:  X[k] = sum_i x[i] alpha_m^(ik).
+template <class FO>
+DEVI void ntt2_lds(const Cfg& cfg, typename FO::T* A, typename FO::T* B, uint32_t tid,
+                   uint32_t nthr) {
+  const uint32_t m = cfg.m, logm = cfg.logm;
+  for (uint32_t st = 1; st <= logm; ++st) {
+    const uint32_t half = 1u << (st - 1);
+    for (uint32_t q = tid; q < m; q += nthr) {  // q < m/2: array A, else array B
+      typename FO::T* a = q < (m >> 1) ? A : B;
+      const uint32_t bq = q & ((m >> 1) - 1u);
+      const uint32_t grp = bq >> (st - 1), k = bq & (half - 1u);
+      const uint32_t i = grp * 2u * half + k, j = i + half;
+      const typename FO::T w = ld_tw<FO>(cfg, k << (logm - st));
+      const typename FO::T u = a[i];
+      const typename FO::T v = FO::mul(w, a[j]);
+      a[i] = FO::add(u, v);
+      a[j] = FO::sub(u, v);
+    }
+    __syncthreads();
+  }
+}
+
+// Block-wide modular sum of one value per thread (all threads call; result valid in all threads).
+template <class FO>
+DEVI typename FO::T block_sum(typename FO::T x, typename FO::T* red, uint32_t tid, uint32_t nthr) {
+  red[tid] = x;
+  __syncthreads();
+  for (uint32_t s = 1; s < nthr; s <<= 1) {
+    typename FO::T y = FO::zero();
+    const bool act = (tid % (2 * s) == 0) && (tid + s < nthr);
+    if (act) y = FO::add(red[tid], red[tid + s]);
+    __syncthreads();
+    if (act) red[tid] = y;
+    __syncthreads();
+  }
+  typename FO::T out = red[0];
+  __syncthreads();
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------------
+// FLP query (prio src/flp.rs Type::query with QueryShimGadget), one block per report.
+//
+// For every wire i:  wire_i(t) = sum_{k=0}^{calls} L_k(t) f_{i,k},  f_{i,0} = proof seed,
+//   L_k(t) = alpha^k (t^m - 1) / (m (t - alpha^k)) = (alpha^k/m) * NTT_m(t^(m-1-i))[k]
+// which equals prio's iDFT + Horner evaluation bit for bit (same polynomial).  The gadget outputs
+// p(alpha^k) come from one size-m NTT of the gadget poly folded mod x^m - 1.
+//
+// ParallelSum(Mul, c) types (SumVec, Histogram), column j, row k, idx = (k-1)c + j:
+//   f_{2j,k}   = r^(idx+1) x_idx  (0 if padded)    -> wire_2j   = L0 s_2j   + r^(j+1) sum_k (L_k r^(c(k-1))) x
+//   f_{2j+1,k} = x_idx - 1/2      (-1/2 if padded) -> wire_2j+1 = L0 s_2j+1 + sum_k L_k x - 1/2 sum_k L_k
+// LDS layout (dynamic):  TP[2m] | NA[m] | NB[m] | LM[m] | MM[m] | RP[c+1] | PA[H*c] | PB[H*c] | RED[nthr] | flag
+// ------------------------------------------------------------------------------------------------
+struct FlpDims {
+  uint32_t H;       // row groups in the main loop
+  uint32_t cols;    // columns (chunk) for ParallelSum, 1 for Sum, 1 for Count
+  uint32_t rp_len;  // entries of the r-power table RP
+};
+
+template <class FO>
+__global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
+                                                   CRows proof, CRows tq, CRows jr, CRows part,
+                                                   Rows out_prep, uint8_t* status) {
+  using T = typename FO::T;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t r = blockIdx.x;
+  if (r >= n) return;
+  if (status[r] != ST_OK) return;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  const uint32_t m = cfg.m, logm = cfg.logm, c = dims.cols, H = dims.H;
+  T* TP = reinterpret_cast<T*>(smem);
+  T* NA = TP + 2 * m;
+  T* NB = NA + m;
+  T* LM = NB + m;
+  T* MM = LM + m;
+  T* RP = MM + m;
+  T* PA = RP + dims.rp_len;
+  T* PB = PA + H * c;
+  T* RED = PB + H * c;
+  uint32_t* flag = reinterpret_cast<uint32_t*>(RED + nthr);
+  if (tid == 0) *flag = 0u;
+
+  const uint8_t* xr = meas.at(r);
+  const uint8_t* pr = proof.at(r);
+  const uint32_t arity = cfg.arity;
+  const uint32_t gp_len = cfg.gp_len;
+
+  // ---- powers of t (Montgomery): TP[i] = t^i, i < 2m ----
+  const T tm = FO::to_mont(FO::load(tq.at(r)));
+  if (tid == 0) {
+    TP[0] = FO::one_mont();
+    TP[1] = tm;
+  }
+  __syncthreads();
+  for (uint32_t s = 2; s < 2 * m; s <<= 1) {
+    const T base = TP[s >> 1];
+    const T b2 = FO::mul(base, base);  // t^s
+    for (uint32_t i = tid; i < s && i + s < 2 * m; i += nthr) TP[i + s] = FO::mul(TP[i], b2);
+    __syncthreads();
+  }
+  // ---- r powers ----
+  T rm = FO::one_mont();
+  if (cfg.jr_len > 0) rm = FO::to_mont(FO::load(jr.at(r)));
+  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
+    // RP[j] = r^(j+1), j < c ; MM[k] (k = 1..calls) = r^(c(k-1)) (stored temporarily)
+    for (uint32_t j = tid; j < c; j += nthr) RP[j] = mont_pow<FO>(rm, j + 1);
+    for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) MM[k] = mont_pow<FO>(rm, (uint64_t)c * (k - 1));
+  } else if (cfg.kind == KIND_SUM) {
+    for (uint32_t k = tid; k <= cfg.calls; k += nthr) RP[k] = mont_pow<FO>(rm, k);  // r^k
+  }
+  // ---- NTT inputs: NA <- t^(m-1-i) (bit-reversed), NB <- folded gadget poly (bit-reversed) ----
+  bool bad = false;
+  for (uint32_t i = tid; i < m; i += nthr) {
+    const uint32_t bi = bitrev(i, logm);
+    NA[bi] = TP[m - 1 - i];
+    T e = FO::load(pr + (size_t)(arity + i) * FO::ES);
+    bad |= !FO::is_canonical(e);
+    if (i + m < gp_len) {
+      const T e2 = FO::load(pr + (size_t)(arity + i + m) * FO::ES);
+      bad |= !FO::is_canonical(e2);
+      e = FO::add(e, e2);
+    }
+    NB[bi] = e;
+  }
+  if (tid == 0 && FO::eq(TP[m], FO::one_mont())) atomicOr(flag, 2u);  // t^m == 1
+  __syncthreads();
+  ntt2_lds<FO>(cfg, NA, NB, tid, nthr);
+  // ---- Lagrange weights (Montgomery): LM[k] = Y_k * alpha^k / m ; MM[k] = LM[k] * r^(c(k-1)) ----
+  const T inv_m = ld_tw<FO>(cfg, m);  // table entry m holds 1/m (Montgomery)
+  for (uint32_t k = tid; k < m; k += nthr) {
+    T y = FO::mul(NA[k], ld_tw<FO>(cfg, k));
+    y = FO::mul(y, inv_m);
+    LM[k] = y;
+  }
+  __syncthreads();
+  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
+    for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) MM[k] = FO::mul(LM[k], MM[k]);
+  }
+  __syncthreads();
+
+  // ---- p(t) = sum_d c_d t^d (canonical), and the circuit's gadget-output combination ----
+  T pt = FO::zero();
+  for (uint32_t d = tid; d < gp_len; d += nthr) {
+    pt = FO::add(pt, FO::mul(TP[d], FO::load(pr + (size_t)(arity + d) * FO::ES)));
+  }
+  T gsum = FO::zero();  // SumVec/Hist: sum_k p(alpha^k) ; Sum: sum_k r^k p(alpha^k) ; Count: p(alpha)
+  T lsum = FO::zero();  // sum_{k=1..calls} L_k (Montgomery)
+  for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) {
+    if (cfg.kind == KIND_SUM) gsum = FO::add(gsum, FO::mul(RP[k], NB[k]));
+    else gsum = FO::add(gsum, NB[k]);
+    lsum = FO::add(lsum, LM[k]);
+  }
+  pt = block_sum<FO>(pt, RED, tid, nthr);
+  gsum = block_sum<FO>(gsum, RED, tid, nthr);
+  lsum = block_sum<FO>(lsum, RED, tid, nthr);
+
+  // ---- main loop: wire accumulations over the measurement share ----
+  T xsum = FO::zero();  // Histogram sum check
+  uint8_t* outp = out_prep.at(r);
+  const size_t ES = FO::ES;
+  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
+    for (uint32_t slot = tid; slot < H * c; slot += nthr) {
+      const uint32_t j = slot % c, h = slot / c;
+      T accA = FO::zero(), accB = FO::zero();
+      for (uint32_t k = 1 + h; k <= cfg.calls; k += H) {
+        const uint32_t idx = (k - 1) * c + j;
+        if (idx < cfg.meas_len) {
+          const T x = FO::load(xr + (size_t)idx * ES);
+          bad |= !FO::is_canonical(x);
+          accA = FO::add(accA, FO::mul(MM[k], x));
+          accB = FO::add(accB, FO::mul(LM[k], x));
+          xsum = FO::add(xsum, x);
+        }
+      }
+      PA[h * c + j] = accA;
+      PB[h * c + j] = accB;
+    }
+    __syncthreads();
+    const T l0 = LM[0];
+    const T half_l = FO::mul(lsum, FO::half());  // (1/2) sum_k L_k, canonical
+    for (uint32_t j = tid; j < c; j += nthr) {
+      T a = FO::zero(), b = FO::zero();
+      for (uint32_t h = 0; h < H; ++h) {
+        a = FO::add(a, PA[h * c + j]);
+        b = FO::add(b, PB[h * c + j]);
+      }
+      const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
+      const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
+      bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
+      const T w0 = FO::add(FO::mul(l0, s0), FO::mul(RP[j], a));
+      const T w1 = FO::sub(FO::add(FO::mul(l0, s1), b), half_l);
+      FO::store(outp + (size_t)(1 + 2 * j) * ES, w0);
+      FO::store(outp + (size_t)(2 + 2 * j) * ES, w1);
+    }
+  } else if (cfg.kind == KIND_SUM) {
+    T acc = FO::zero();
+    for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) {
+      const T x = FO::load(xr + (size_t)(k - 1) * ES);
+      bad |= !FO::is_canonical(x);
+      acc = FO::add(acc, FO::mul(LM[k], x));
+    }
+    acc = block_sum<FO>(acc, RED, tid, nthr);
+    if (tid == 0) {
+      const T s0 = FO::load(pr);
+      bad |= !FO::is_canonical(s0);
+      FO::store(outp + 1 * ES, FO::add(FO::mul(LM[0], s0), acc));
+    }
+  } else {  // KIND_COUNT: wires f_{0,1} = f_{1,1} = x0
+    if (tid == 0) {
+      const T x = FO::load(xr);
+      bad |= !FO::is_canonical(x);
+      xsum = x;
+      const T lx = FO::mul(LM[1], x);
+      for (uint32_t w = 0; w < 2; ++w) {
+        const T s = FO::load(pr + (size_t)w * ES);
+        bad |= !FO::is_canonical(s);
+        FO::store(outp + (size_t)(1 + w) * ES, FO::add(FO::mul(LM[0], s), lx));
+      }
+    }
+  }
+  if (bad) atomicOr(flag, 1u);
+  if (cfg.kind == KIND_HISTOGRAM) xsum = block_sum<FO>(xsum, RED, tid, nthr);
+  __syncthreads();
+  if (tid == 0) {
+    T v;
+    if (cfg.kind == KIND_COUNT) {
+      v = FO::sub(gsum, xsum);
+    } else if (cfg.kind == KIND_HISTOGRAM) {
+      // jr[1] * range + jr[1]^2 * (sum x - 1/2)
+      const T r1m = FO::to_mont(FO::load(jr.at(r) + ES));
+      const T sc = FO::sub(xsum, FO::half());
+      v = FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc));
+    } else {
+      v = gsum;
+    }
+    FO::store(outp, v);
+    FO::store(outp + (size_t)(1 + arity) * ES, pt);
+    if (cfg.jr_len > 0) {
+      const uint8_t* pp = part.at(r);
+      uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
+      st64(dst, ld64(pp));
+      st64(dst + 8, ld64(pp + 8));
+    }
+    const uint32_t f = *flag;
+    if (f & 1u) status[r] = ST_INVALID_MESSAGE;
+    else if (f & 2u) status[r] = ST_VDAF_PREP_ERROR;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// prepare_shares_to_prepare_message (prio): verifier = sum of shares; decide; msg = derive_seed(
+// 0^16, dst6, part_0 || part_1).  decide: v == 0 and G(wires) == p(t),
+//   G = Mul / ParallelSum(Mul): sum_j w_2j w_2j+1 ;  PolyEval(x^2 - x): w^2 - w.
+// ------------------------------------------------------------------------------------------------
+template <class FO>
+__global__ void __launch_bounds__(256) k_decide(Cfg cfg, uint32_t n, CRows leader_prep,
+                                                CRows helper_prep, Rows out_msg, uint8_t* status) {
+  using T = typename FO::T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (status[r] != ST_OK) return;
+  const uint8_t* a = leader_prep.at(r);
+  const uint8_t* b = helper_prep.at(r);
+  const size_t ES = FO::ES;
+  bool bad = false;
+  auto vsum = [&](uint32_t i) -> T {
+    const T x = FO::load(a + i * ES), y = FO::load(b + i * ES);
+    bad |= !FO::is_canonical(x) || !FO::is_canonical(y);
+    return FO::add(x, y);
+  };
+  const T v = vsum(0);
+  T g = FO::zero();
+  if (cfg.kind == KIND_SUM) {
+    const T w = vsum(1);
+    g = FO::sub(FO::mul(FO::to_mont(w), w), w);
+  } else {
+    for (uint32_t j = 0; j < cfg.arity / 2; ++j) {
+      const T w0 = vsum(1 + 2 * j), w1 = vsum(2 + 2 * j);
+      g = FO::add(g, FO::mul(FO::to_mont(w0), w1));
+    }
+  }
+  const T pt = vsum(1 + cfg.arity);
+  bool ok = !bad && FO::is_zero(v) && FO::eq(g, pt);
+  if (!ok) {
+    status[r] = ST_VDAF_PREP_ERROR;
+    return;
+  }
+  if (cfg.jr_len > 0) {
+    const uint8_t* pa = a + (size_t)cfg.verifier_len * ES;
+    const uint8_t* pb = b + (size_t)cfg.verifier_len * ES;
+    uint64_t lo, hi;
+    derive_jr_seed(cfg.algo_id, ld64(pa), ld64(pa + 8), ld64(pb), ld64(pb + 8), lo, hi);
+    st64(out_msg.at(r), lo);
+    st64(out_msg.at(r) + 8, hi);
+  }
+}
+
+// prepare_next (prio): the prep msg must equal the corrected joint-rand seed.
+__global__ void __launch_bounds__(256) k_prepare_next(Cfg cfg, uint32_t n, CRows msgs, CRows seeds,
+                                                      uint8_t* status) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (status[r] != ST_OK || cfg.jr_len == 0) return;
+  const uint8_t* a = msgs.at(r);
+  const uint8_t* b = seeds.at(r);
+  if (ld64(a) != ld64(b) || ld64(a + 8) != ld64(b + 8)) status[r] = ST_VDAF_PREP_ERROR;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Output shares and aggregation (prio Type::truncate + Aggregatable::accumulate; Janus
+// Accumulator::update accumulator.rs:76-122 / BatchAggregation::merged_with models.rs:962-991).
+// ------------------------------------------------------------------------------------------------
+template <class FO>
+DEVI typename FO::T out_elem(const Cfg& cfg, const uint8_t* x, uint32_t e) {
+  using T = typename FO::T;
+  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_SUM) {
+    // sum_b 2^b x_b over `bits` consecutive elements, Horner from the top bit
+    const uint8_t* p = x + (size_t)e * cfg.bits * FO::ES;
+    T acc = FO::zero();
+    for (int b = (int)cfg.bits - 1; b >= 0; --b) {
+      acc = FO::add(FO::dbl(acc), FO::load(p + (size_t)b * FO::ES));
+    }
+    return acc;
+  }
+  return FO::load(x + (size_t)e * FO::ES);
+}
+
+// Segmented partial sums.  chunk c covers perm[chunk_begin[c] .. chunk_begin[c+1]); all reports of
+// a chunk share one batch slot.  Block (chunk, elem-tile): EPB elements x G report groups.
+template <class FO>
+__global__ void __launch_bounds__(256) k_accum_partial(Cfg cfg, CRows meas, const uint32_t* perm,
+                                                       const uint32_t* chunk_begin,
+                                                       const uint8_t* status, uint32_t epb,
+                                                       uint8_t* partials, uint32_t* part_counts) {
+  using T = typename FO::T;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  T* red = reinterpret_cast<T*>(smem);
+  const uint32_t ch = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t G = blockDim.x / epb;
+  const uint32_t el = tid % epb, g = tid / epb;
+  const uint32_t e = blockIdx.y * epb + el;
+  const uint32_t b0 = chunk_begin[ch], b1 = chunk_begin[ch + 1];
+  T acc = FO::zero();
+  uint32_t cnt = 0;
+  if (g < G && e < cfg.out_len) {
+    for (uint32_t i = b0 + g; i < b1; i += G) {
+      const uint32_t r = perm[i];
+      if (status[r] != ST_OK) continue;
+      acc = FO::add(acc, out_elem<FO>(cfg, meas.at(r), e));
+      ++cnt;
+    }
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (g == 0 && e < cfg.out_len) {
+    T s = acc;
+    for (uint32_t q = 1; q < G; ++q) s = FO::add(s, red[q * epb + el]);
+    FO::store(partials + ((size_t)ch * cfg.out_len + e) * FO::ES, s);
+  }
+  if (blockIdx.y == 0) {
+    // report count for this chunk (independent of element)
+    __syncthreads();
+    uint32_t* rc = reinterpret_cast<uint32_t*>(smem);
+    if (tid == 0) *rc = 0;
+    __syncthreads();
+    if (el == 0 && cfg.out_len > 0) atomicAdd(rc, cnt);
+    __syncthreads();
+    if (tid == 0) part_counts[ch] = *rc;
+  }
+}
+
+// agg[slot(c)] += partial[c] for every chunk c, in chunk order (deterministic).  Chunks of one
+// slot are contiguous, so each thread keeps a register sum per slot run.
+template <class FO>
+__global__ void __launch_bounds__(256) k_accum_merge(Cfg cfg, uint32_t nchunks,
+                                                     const uint32_t* chunk_slot,
+                                                     const uint8_t* partials,
+                                                     const uint32_t* part_counts, uint8_t* agg,
+                                                     unsigned long long* counts) {
+  using T = typename FO::T;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < cfg.out_len) {
+    uint32_t c = 0;
+    while (c < nchunks) {
+      const uint32_t slot = chunk_slot[c];
+      T acc = FO::zero();
+      uint32_t c1 = c;
+      while (c1 < nchunks && chunk_slot[c1] == slot) ++c1;
+#pragma unroll 8
+      for (uint32_t q = c; q < c1; ++q)
+        acc = FO::add(acc, FO::load(partials + ((size_t)q * cfg.out_len + e) * FO::ES));
+      uint8_t* dst = agg + ((size_t)slot * cfg.out_len + e) * FO::ES;
+      FO::store(dst, FO::add(FO::load(dst), acc));
+      c = c1;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (uint32_t c = 0; c < nchunks; ++c) counts[chunk_slot[c]] += part_counts[c];
+  }
+}
+
+// Per-report output shares (optional debugging/parity output of prepare_next).
+template <class FO>
+__global__ void __launch_bounds__(256) k_out_shares(Cfg cfg, uint32_t n, CRows meas,
+                                                    Rows out, const uint8_t* status) {
+  const uint32_t r = blockIdx.y;
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n || e >= cfg.out_len) return;
+  typename FO::T v = FO::zero();
+  if (status[r] == ST_OK) v = out_elem<FO>(cfg, meas.at(r), e);
+  FO::store(out.at(r) + (size_t)e * FO::ES, v);
+}
+
+// dst[i] += src[i] (mod p) over `nelems` field elements (RCCL all-gather merge, K6).
+template <class FO>
+__global__ void __launch_bounds__(256) k_merge(uint8_t* dst, const uint8_t* src, size_t nelems) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nelems) return;
+  FO::store(dst + i * FO::ES, FO::add(FO::load(dst + i * FO::ES), FO::load(src + i * FO::ES)));
+}
+
+}  // namespace p3g

@@ -1,0 +1,314 @@
+"""Host-side mirror of prio 0.15.1's `prio::vdaf::{Aggregator, Collector}` surface for Prio3,
+batched over whole aggregation jobs and executed by the MI355X HIP engine (libprio3gpu.so).
+
+Reference surface:
+  * `Prio3::new_count / new_sum / new_sum_vec / new_histogram` as constructed by Janus at
+    `aggregator/src/aggregator.rs:797-840`; chunk length = floor(sqrt(len)) (`core/src/task.rs:84-86`).
+  * `Aggregator::prepare_init`, `prepare_shares_to_prepare_message`, `prepare_next`, `aggregate`
+    (fake-VDAF mirror: `core/src/test_util/dummy_vdaf.rs:80-141`).
+  * `Aggregatable::merge` (`dummy_vdaf.rs:230-242`), `Collector::unshard` (`collector/src/lib.rs:539`).
+  * Per-report errors map to `PrepareError` (`aggregator/src/aggregator/error.rs:240-300`,
+    `messages/src/lib.rs:2288-2298`); one bad report never fails the batch.
+
+Inputs are (n, len) uint8 arrays (numpy, host) or torch uint8 tensors on the GPU (device pointers
+are used directly, no PCIe copy).  There is no CPU fallback: without the HIP library every call
+raises `Prio3GpuError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import Prio3GpuError, check, lib
+
+COUNT, SUM, SUMVEC, HISTOGRAM = 0, 1, 2, 3
+STATUS_OK, STATUS_VDAF_PREP_ERROR, STATUS_INVALID_MESSAGE = 0, 5, 8
+
+FIELD64_MODULUS = 2**64 - 2**32 + 1
+FIELD128_MODULUS = 2**128 - 28 * 2**64 + 1
+
+
+class _Sizes(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "field_size", "meas_len", "proof_len", "verifier_len", "joint_rand_len", "output_len",
+        "leader_input_share", "helper_input_share", "public_share", "prep_share", "prep_msg",
+        "aggregate_share")]
+
+
+def chunk_size(measurement_length: int) -> int:
+    """Janus `VdafInstance::chunk_size` (core/src/task.rs:84-86): floor(sqrt(len))."""
+    return int(math.floor(math.sqrt(measurement_length)))
+
+
+def _ptr(a) -> Optional[int]:
+    """Raw pointer of a numpy array or torch tensor (host or device)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("arrays must be C-contiguous")
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        if not a.is_contiguous():
+            raise ValueError("tensors must be contiguous")
+        return a.data_ptr()
+    raise TypeError(f"unsupported buffer type {type(a)}")
+
+
+def _nbytes(a) -> int:
+    if isinstance(a, np.ndarray):
+        return a.nbytes
+    return a.numel() * a.element_size()
+
+
+def _as_u8(a, n: int, width: int, what: str):
+    if a is None:
+        return None
+    if isinstance(a, (bytes, bytearray)):
+        a = np.frombuffer(bytes(a), dtype=np.uint8)
+    if isinstance(a, (list, tuple)):
+        a = np.frombuffer(b"".join(a), dtype=np.uint8)
+    if _nbytes(a) != n * width:
+        raise ValueError(f"{what}: expected {n}x{width} bytes, got {_nbytes(a)}")
+    if isinstance(a, np.ndarray):
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a
+
+
+class PrepareState:
+    """Batch `Prio3PrepareState` for one aggregator (device scratch for up to `capacity`)."""
+
+    def __init__(self, vdaf: "Prio3Gpu", agg_id: int, capacity: int):
+        self.vdaf, self.agg_id, self.capacity = vdaf, agg_id, capacity
+        h = ctypes.c_void_p()
+        check(lib().prio3gpu_state_create(vdaf._ctx, agg_id, capacity, ctypes.byref(h)),
+              "state_create")
+        self._h = h
+        self._keep = None  # keeps device inputs referenced until prepare_next
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().prio3gpu_state_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class AggregateShares:
+    """Per-batch-identifier aggregate shares kept in HBM (`num_slots` batch identifiers)."""
+
+    def __init__(self, vdaf: "Prio3Gpu", num_slots: int = 1):
+        self.vdaf, self.num_slots = vdaf, num_slots
+        h = ctypes.c_void_p()
+        check(lib().prio3gpu_agg_create(vdaf._ctx, num_slots, ctypes.byref(h)), "agg_create")
+        self._h = h
+
+    def reset(self):
+        check(lib().prio3gpu_agg_reset(self._h), "agg_reset")
+
+    def read(self, slot: int = 0):
+        """(aggregate share bytes, report count) for one batch slot."""
+        out = np.zeros(self.vdaf.sizes.aggregate_share, dtype=np.uint8)
+        cnt = ctypes.c_uint64()
+        check(lib().prio3gpu_agg_read(self._h, slot, _ptr(out), ctypes.byref(cnt)), "agg_read")
+        return out.tobytes(), cnt.value
+
+    def merge(self, slot: int, share: bytes, count: int):
+        """`Aggregatable::merge` with an encoded aggregate share."""
+        buf = np.frombuffer(bytes(share), dtype=np.uint8).copy()
+        check(lib().prio3gpu_agg_merge_bytes(self._h, slot, _ptr(buf), count), "agg_merge")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().prio3gpu_agg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Prio3Gpu:
+    """Prio3 with NUM_SHARES = 2 bound to one verify key (one Janus task) and one GPU."""
+
+    def __init__(self, kind: int, verify_key: bytes, bits: int = 0, length: int = 0,
+                 chunk_length: int = 0, device: int = 0):
+        if len(verify_key) != 16:
+            raise ValueError("verify key must be 16 bytes")
+        self.kind, self.bits, self.length, self.chunk_length = kind, bits, length, chunk_length
+        self.verify_key = bytes(verify_key)
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().prio3gpu_ctx_create(kind, bits, length, chunk_length, self.verify_key, device,
+                                        ctypes.byref(h)), "ctx_create")
+        self._ctx = h
+        s = _Sizes()
+        check(lib().prio3gpu_ctx_sizes(self._ctx, ctypes.byref(s)), "ctx_sizes")
+        self.sizes = s
+        self.modulus = FIELD64_MODULUS if s.field_size == 8 else FIELD128_MODULUS
+
+    # -- constructors mirroring prio (Janus passes num_aggregators = 2) -------------------------
+    @classmethod
+    def new_count(cls, verify_key, device=0):
+        return cls(COUNT, verify_key, device=device)
+
+    @classmethod
+    def new_sum(cls, bits, verify_key, device=0):
+        return cls(SUM, verify_key, bits=bits, device=device)
+
+    @classmethod
+    def new_sum_vec(cls, bits, length, chunk_length, verify_key, device=0):
+        return cls(SUMVEC, verify_key, bits=bits, length=length, chunk_length=chunk_length,
+                   device=device)
+
+    @classmethod
+    def new_count_vec(cls, length, chunk_length, verify_key, device=0):
+        """Janus `Prio3CountVec` = SumVec with bits = 1 (aggregator.rs:805-813)."""
+        return cls.new_sum_vec(1, length, chunk_length, verify_key, device)
+
+    @classmethod
+    def new_histogram(cls, length, chunk_length, verify_key, device=0):
+        return cls(HISTOGRAM, verify_key, length=length, chunk_length=chunk_length, device=device)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib().prio3gpu_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream(self) -> int:
+        return lib().prio3gpu_ctx_stream(self._ctx) or 0
+
+    def sync(self):
+        check(lib().prio3gpu_ctx_sync(self._ctx), "sync")
+
+    def new_state(self, agg_id: int, capacity: int) -> PrepareState:
+        return PrepareState(self, agg_id, capacity)
+
+    def new_aggregate(self, num_slots: int = 1) -> AggregateShares:
+        return AggregateShares(self, num_slots)
+
+    # -- Aggregator --------------------------------------------------------------------------------
+    def prepare_init(self, state: PrepareState, nonces, public_shares, input_shares,
+                     status=None, want_prep_shares: bool = True):
+        """Batched `prepare_init` -> (prep_shares (n, prep_share) uint8, status (n,) uint8)."""
+        s = self.sizes
+        n = _nbytes(nonces) // 16
+        in_len = s.leader_input_share if state.agg_id == 0 else s.helper_input_share
+        nonces = _as_u8(nonces, n, 16, "nonces")
+        public_shares = _as_u8(public_shares, n, s.public_share, "public shares") \
+            if s.public_share else None
+        input_shares = _as_u8(input_shares, n, in_len, "input shares")
+        st = np.zeros(n, dtype=np.uint8) if status is None else status
+        prep = np.zeros((n, s.prep_share), dtype=np.uint8) if want_prep_shares else None
+        check(lib().prio3gpu_prepare_init(self._ctx, state._h, n, _ptr(nonces),
+                                          _ptr(public_shares), _ptr(input_shares), _ptr(prep),
+                                          _ptr(st)), "prepare_init")
+        state._keep = input_shares
+        return prep, st
+
+    def prepare_shares_to_prepare_message(self, leader_prep_shares, helper_prep_shares,
+                                          status=None):
+        s = self.sizes
+        n = _nbytes(leader_prep_shares) // s.prep_share
+        lp = _as_u8(leader_prep_shares, n, s.prep_share, "leader prep shares")
+        hp = _as_u8(helper_prep_shares, n, s.prep_share, "helper prep shares")
+        st = np.zeros(n, dtype=np.uint8) if status is None else status
+        msgs = np.zeros((n, max(1, s.prep_msg)), dtype=np.uint8)[:, :s.prep_msg].copy()
+        check(lib().prio3gpu_prepare_shares_to_prepare_message(
+            self._ctx, n, _ptr(lp), _ptr(hp), _ptr(msgs) if s.prep_msg else None, _ptr(st)),
+            "prepare_shares_to_prepare_message")
+        return msgs, st
+
+    def prepare_next(self, state: PrepareState, prep_msgs, status, want_output_shares=True,
+                     agg: Optional[AggregateShares] = None, batch_slots=None):
+        s = self.sizes
+        n = _nbytes(status)
+        msgs = _as_u8(prep_msgs, n, s.prep_msg, "prep msgs") if s.prep_msg else None
+        outs = np.zeros((n, s.aggregate_share), dtype=np.uint8) if want_output_shares else None
+        slots = None
+        if batch_slots is not None:
+            slots = batch_slots if not isinstance(batch_slots, np.ndarray) else \
+                np.ascontiguousarray(batch_slots, dtype=np.uint32)
+        check(lib().prio3gpu_prepare_next(self._ctx, state._h, n, _ptr(msgs), _ptr(status),
+                                          _ptr(outs), _ptr(slots), agg._h if agg else None),
+              "prepare_next")
+        return outs, status
+
+    def helper_init(self, state: PrepareState, nonces, public_shares, helper_input_shares,
+                    leader_prep_shares, agg: Optional[AggregateShares] = None, batch_slots=None,
+                    status=None, out_prep_msgs=None):
+        """Helper aggregate-init for a whole job (aggregator.rs:1613-1848): returns
+        (prep_msgs, status); output shares are accumulated into `agg`."""
+        s = self.sizes
+        n = _nbytes(nonces) // 16
+        nonces = _as_u8(nonces, n, 16, "nonces")
+        pub = _as_u8(public_shares, n, s.public_share, "public shares") if s.public_share else None
+        hs = _as_u8(helper_input_shares, n, s.helper_input_share, "helper input shares")
+        lp = _as_u8(leader_prep_shares, n, s.prep_share, "leader prep shares")
+        st = np.zeros(n, dtype=np.uint8) if status is None else status
+        msgs = out_prep_msgs
+        if msgs is None and s.prep_msg:
+            msgs = np.zeros((n, s.prep_msg), dtype=np.uint8)
+        slots = None
+        if batch_slots is not None:
+            slots = batch_slots if not isinstance(batch_slots, np.ndarray) else \
+                np.ascontiguousarray(batch_slots, dtype=np.uint32)
+        check(lib().prio3gpu_helper_init(self._ctx, state._h, n, _ptr(nonces), _ptr(pub),
+                                         _ptr(hs), _ptr(lp), _ptr(slots), _ptr(msgs), _ptr(st),
+                                         agg._h if agg else None), "helper_init")
+        return msgs, st
+
+    # -- Collector ---------------------------------------------------------------------------------
+    def decode_field_vec(self, b: bytes):
+        es = self.sizes.field_size
+        return [int.from_bytes(b[i:i + es], "little") for i in range(0, len(b), es)]
+
+    def unshard(self, aggregate_shares: Sequence[bytes]):
+        """`Collector::unshard`: sum the two aggregate shares and decode the result."""
+        p = self.modulus
+        vecs = [self.decode_field_vec(a) for a in aggregate_shares]
+        out = [sum(col) % p for col in zip(*vecs)]
+        if self.kind in (COUNT, SUM):
+            return out[0]
+        return out
+
+
+class Comm:
+    """RCCL communicator for the per-GPU partial-aggregate merge (one process per GPU)."""
+
+    def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int):
+        h = ctypes.c_void_p()
+        buf = np.frombuffer(bytes(unique_id), dtype=np.uint8).copy()
+        check(lib().prio3gpu_comm_init(_ptr(buf), nranks, rank, device, ctypes.byref(h)),
+              "comm_init")
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = np.zeros(128, dtype=np.uint8)
+        check(lib().prio3gpu_comm_unique_id(_ptr(buf)), "comm_unique_id")
+        return buf.tobytes()
+
+    def allreduce(self, vdaf: Prio3Gpu, agg: AggregateShares):
+        check(lib().prio3gpu_agg_allreduce(self._h, vdaf._ctx, agg._h), "agg_allreduce")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().prio3gpu_comm_destroy(self._h)
+            self._h = None

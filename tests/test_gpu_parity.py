@@ -1,0 +1,207 @@
+"""GPU parity: the HIP engine (through the C ABI) vs the CPU oracle, bit-exact.
+
+Every byte the reference path produces per report -- prep shares (both aggregators), prep
+messages, output shares, aggregate shares -- is compared with the oracle's VdafTranscript
+(core/src/test_util/mod.rs:50-233).  Negative cases follow the reference's per-report error
+mapping (aggregator/src/aggregator/error.rs:240-300): a bad report is rejected alone.
+"""
+import numpy as np
+import pytest
+
+from tests.reports import CONFIGS, expected_aggregate, make_batch, plaintext_sum
+
+pytestmark = pytest.mark.gpu
+
+SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
+         "hist256": 24, "sumvec_8_1000": 6}
+
+_cache = {}
+
+
+def batch(name):
+    if name not in _cache:
+        _cache[name] = make_batch(name, SIZES[name])
+    return _cache[name]
+
+
+def gpu_vdaf(b):
+    from janus_amd.prio3 import Prio3Gpu
+    c = CONFIGS[b.name]
+    return Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"], length=c["length"],
+                    chunk_length=c["chunk"])
+
+
+@pytest.mark.parametrize("name", list(SIZES))
+def test_prepare_transcript_bit_exact(name):
+    b = batch(name)
+    v = gpu_vdaf(b)
+    s = v.sizes
+    assert s.leader_input_share == b.leader_in.shape[1]
+    assert s.prep_share == b.leader_prep.shape[1]
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    assert (lst == 0).all()
+    np.testing.assert_array_equal(lp, b.leader_prep)
+    hp, hst = v.prepare_init(hs, b.nonces, b.public, b.helper_in)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(hp, b.helper_prep)
+    msgs, st = v.prepare_shares_to_prepare_message(lp, hp)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(msgs, b.prep_msg)
+    lo, lst = v.prepare_next(ls, msgs, lst.copy())
+    ho, hst = v.prepare_next(hs, msgs, hst.copy())
+    assert (lst == 0).all() and (hst == 0).all()
+    np.testing.assert_array_equal(lo, b.leader_out)
+    np.testing.assert_array_equal(ho, b.helper_out)
+
+
+@pytest.mark.parametrize("name", list(SIZES))
+def test_aggregate_and_unshard(name):
+    b = batch(name)
+    v = gpu_vdaf(b)
+    ls = v.new_state(0, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    # helper: fused aggregate-init
+    hs = v.new_state(1, b.n)
+    hagg = v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, b.nonces, b.public, b.helper_in, lp, agg=hagg)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(msgs, b.prep_msg)
+    lagg = v.new_aggregate(1)
+    v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
+    la, lc = lagg.read(0)
+    ha, hc = hagg.read(0)
+    assert lc == hc == b.n
+    assert la == expected_aggregate(b, "leader")[0]
+    assert ha == expected_aggregate(b, "helper")[0]
+    assert v.unshard([la, ha]) == plaintext_sum(b)
+
+
+@pytest.mark.parametrize("name", ["sum8", "hist4", "sumvec_small", "count"])
+def test_batch_slots_segmentation(name):
+    b = batch(name)
+    v = gpu_vdaf(b)
+    rng = np.random.default_rng(7)
+    slots = rng.integers(0, 3, size=b.n).astype(np.uint32)
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    hagg = v.new_aggregate(3)
+    msgs, hst = v.helper_init(hs, b.nonces, b.public, b.helper_in, lp, agg=hagg,
+                              batch_slots=slots)
+    lagg = v.new_aggregate(3)
+    v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg, batch_slots=slots)
+    for s in range(3):
+        for agg, which in ((lagg, "leader"), (hagg, "helper")):
+            got, cnt = agg.read(s)
+            exp, ecnt = expected_aggregate(b, which, slots=slots, slot=s)
+            assert got == exp and cnt == ecnt
+
+
+def _oracle_prep_share(b, agg_id, r, leader_in=None, public=None):
+    v = b.vdaf
+    share_b = (leader_in if leader_in is not None else b.leader_in)[r].tobytes() if agg_id == 0 \
+        else b.helper_in[r].tobytes()
+    share = v.decode_input_share(agg_id, share_b)
+    pub = v.decode_public_share((public if public is not None else b.public)[r].tobytes())
+    _, ps = v.prepare_init(b.verify_key, agg_id, b.nonces[r].tobytes(), pub, share)
+    return v.encode_prep_share(ps)
+
+
+@pytest.mark.parametrize("name", ["sum8", "hist4", "sumvec_small", "count"])
+def test_tampered_reports_rejected_alone(name):
+    """A tampered leader measurement share fails decide for that report only; the GPU prep
+    shares of the tampered report still match the oracle bit for bit."""
+    b = batch(name)
+    v = gpu_vdaf(b)
+    es = b.vdaf.fld.ENCODED_SIZE
+    bad = [1, 5]
+    lin = b.leader_in.copy()
+    for r in bad:
+        x = int.from_bytes(lin[r, :es].tobytes(), "little")
+        x = (x + 1) % b.vdaf.fld.MODULUS
+        lin[r, :es] = np.frombuffer(x.to_bytes(es, "little"), dtype=np.uint8)
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, lin)
+    assert (lst == 0).all()
+    for r in bad:
+        assert lp[r].tobytes() == _oracle_prep_share(b, 0, r, leader_in=lin)
+    hagg = v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, b.nonces, b.public, b.helper_in, lp, agg=hagg)
+    mask = np.ones(b.n, dtype=bool)
+    mask[bad] = False
+    assert (hst[bad] == 5).all() and (hst[mask] == 0).all()
+    ha, hc = hagg.read(0)
+    exp, ecnt = expected_aggregate(b, "helper", mask=mask)
+    assert ha == exp and hc == ecnt
+
+
+def test_noncanonical_leader_share_is_invalid_message():
+    b = batch("hist4")
+    v = gpu_vdaf(b)
+    lin = b.leader_in.copy()
+    lin[3, :16] = 0xFF  # >= p: decode error
+    ls = v.new_state(0, b.n)
+    _, lst = v.prepare_init(ls, b.nonces, b.public, lin)
+    assert lst[3] == 8 and (np.delete(lst, 3) == 0).all()
+
+
+def test_tampered_public_share_rejected():
+    b = batch("sum8")
+    v = gpu_vdaf(b)
+    pub = b.public.copy()
+    pub[2, 20] ^= 1  # helper's joint-rand part as seen by the leader
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, pub, b.leader_in)
+    assert lp[2].tobytes() == _oracle_prep_share(b, 0, 2, public=pub)
+    hp, hst = v.prepare_init(hs, b.nonces, pub, b.helper_in)
+    assert hp[2].tobytes() == _oracle_prep_share(b, 1, 2, public=pub)
+    msgs, st = v.prepare_shares_to_prepare_message(lp, hp)
+    # helper's part is honest, so prep msg == H(part_L, part_H) is the honest one, but the
+    # leader's corrected seed used the tampered part: decide fails (different joint rand)
+    assert st[2] == 5 and (np.delete(st, 2) == 0).all()
+
+
+def test_wrong_prep_msg_fails_prepare_next():
+    b = batch("sumvec_small")
+    v = gpu_vdaf(b)
+    ls = v.new_state(0, b.n)
+    _, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    msgs = b.prep_msg.copy()
+    msgs[4, 0] ^= 0x80
+    lagg = v.new_aggregate(1)
+    _, st = v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
+    assert st[4] == 5 and (np.delete(st, 4) == 0).all()
+    _, cnt = lagg.read(0)
+    assert cnt == b.n - 1
+
+
+def test_empty_batch():
+    b = batch("sum8")
+    v = gpu_vdaf(b)
+    ls = v.new_state(0, 4)
+    prep, st = v.prepare_init(ls, np.zeros((0, 16), np.uint8), np.zeros((0, 32), np.uint8),
+                              np.zeros((0, v.sizes.leader_input_share), np.uint8))
+    assert prep.shape == (0, v.sizes.prep_share) and st.shape == (0,)
+
+
+def test_device_resident_inputs_torch():
+    import torch
+    b = batch("hist256")
+    v = gpu_vdaf(b)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    ls = v.new_state(0, b.n)
+    lp, lst = v.prepare_init(ls, t(b.nonces), t(b.public), t(b.leader_in))
+    np.testing.assert_array_equal(lp, b.leader_prep)
+
+
+def test_agg_merge_bytes():
+    b = batch("hist4")
+    v = gpu_vdaf(b)
+    agg = v.new_aggregate(2)
+    exp, _ = expected_aggregate(b, "leader")
+    agg.merge(1, exp, 7)
+    agg.merge(1, exp, 3)
+    got, cnt = agg.read(1)
+    x = v.decode_field_vec(exp)
+    assert v.decode_field_vec(got) == [(2 * a) % v.modulus for a in x] and cnt == 10
