@@ -1,0 +1,289 @@
+#!/usr/bin/env python3
+"""Bench: reports/sec prepared+aggregated, Prio3SumVec(bits=8, length=1000, chunk=89), 1..N GPUs.
+
+One "step" = one batch of B synthetic reports per GPU (weak scaling) taken through Janus's whole
+aggregate-init hot path on the GPU: leader prepare_init (aggregation_job_driver.rs:362-380), helper
+prepare_init + prep_shares_to_prep + prepare_next + accumulate (aggregator.rs:1775-1819), leader
+prepare_next + accumulate (aggregation_job_driver.rs:579-627).  For N > 1 every step ends with the
+RCCL all-gather + mod-p merge of both aggregators' per-GPU partial aggregate shares.  Inputs
+(decrypted shares, SURVEY.md §8(d) recipe) are resident in HBM before timing starts; HPKE is out of
+scope.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]  (N > 1 via torch.distributed.run).
+Prints one JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (kind, bits, length, chunk, metric label)
+    "sumvec": (2, 8, 1000, 89, "Prio3SumVec bits=8 length=1000 chunk=89"),
+    "sum": (1, 32, 0, 0, "Prio3Sum bits=32"),
+    "histogram": (3, 0, 256, 16, "Prio3Histogram length=256 chunk=16"),
+    "count": (0, 0, 0, 0, "Prio3Count"),
+}
+METRIC = "reports/sec prepared+aggregated, Prio3SumVec len=1000, 1/2/4/8 GPUs"
+
+# gfx950 peaks (MI355X_MICROARCH.md): FP32 vector 157.3 TFLOP/s = 256 CU x 128 lanes/clk x 2.4 GHz
+# x 2 (FMA)  ->  int32 VALU 78.6 Tops/s;  HBM3E 8.0 TB/s.
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0
+# SURVEY.md §8(d) declared cost model: 7,440 int32 VALU ops per Keccak-f[1600]; 36 per F128 mul.
+OPS_PER_PERM = 7440
+
+
+def perms_per_report(kind_name, sizes):
+    """Keccak-f[1600] permutations per report executed by each XOF kernel (one aggregator)."""
+    es = sizes.field_size
+
+    def squeeze(nelem):
+        return max(1, math.ceil(nelem * es / 168))
+
+    jr = sizes.joint_rand_len
+    part = math.ceil((42 + sizes.meas_len * es + 1) / 168) if jr else 0
+    return {
+        "k_query_rand": 1,
+        "k_expand": squeeze(sizes.meas_len) + squeeze(sizes.proof_len),
+        "k_jr": (part + 1 + squeeze(jr)) if jr else 0,
+        "k_decide": 1 if jr else 0,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="sumvec", choices=list(CONFIGS))
+    ap.add_argument("--reports", type=int, default=0, help="reports per GPU per step (B)")
+    ap.add_argument("--unique", type=int, default=0, help="distinct synthetic reports per rank")
+    ap.add_argument("--gen-threads", type=int, default=16)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from janus_amd import _lib
+    from janus_amd._lib import check, lib
+    from janus_amd.prio3 import Comm, Prio3Gpu
+    from oracle.ref import Prio3Ref
+
+    kind, bits, length, chunk, label = CONFIGS[args.config]
+    defaults = {"sumvec": (65536, 8192), "sum": (1 << 20, 16384), "histogram": (1 << 20, 16384),
+                "count": (1 << 22, 65536)}
+    B = args.reports or defaults[args.config][0]
+    U = args.unique or defaults[args.config][1]
+    U = min(U, B)
+    if B % U:
+        B = (B // U) * U
+    cfg_id = f"bench-{args.config}".encode()
+    import hashlib
+    vk = hashlib.shake_128(b"verify-key" + cfg_id).digest(16)
+
+    vdaf = Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=local_rank)
+    s = vdaf.sizes
+
+    # ---- synthetic inputs: U distinct reports per rank (C restatement client), tiled to B ------
+    ref = Prio3Ref(kind, vk, bits, length, chunk)
+    t0 = time.time()
+    gen = ref.gen(cfg_id, rank * U, U, threads=args.gen_threads)
+    gen_s = time.time() - t0
+    tiles = B // U
+
+    def to_dev(a):
+        t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        return t.repeat(tiles, *([1] * (t.dim() - 1))).contiguous() if tiles > 1 else t
+
+    d_nonces = to_dev(gen["nonces"])
+    d_pub = to_dev(gen["public"]) if s.public_share else None
+    d_lin = to_dev(gen["leader_in"])
+    d_hin = to_dev(gen["helper_in"])
+    d_lprep = torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
+    d_msgs = torch.empty((B, max(1, s.prep_msg)), dtype=torch.uint8, device=dev)
+    d_lst = torch.zeros(B, dtype=torch.uint8, device=dev)
+    d_hst = torch.zeros(B, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    ls, hs = vdaf.new_state(0, B), vdaf.new_state(1, B)
+    lagg, hagg = vdaf.new_aggregate(1), vdaf.new_aggregate(1)
+    comm = None
+    if world > 1:
+        uid = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm(uid[0], world, rank, local_rank)
+    L = lib()
+    ctx = vdaf._ctx
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def step():
+        d_lst.zero_()
+        d_hst.zero_()
+        torch.cuda.synchronize()
+        check(L.prio3gpu_prepare_init(ctx, ls._h, B, P(d_nonces), P(d_pub), P(d_lin), P(d_lprep),
+                                      P(d_lst)), "leader prepare_init")
+        check(L.prio3gpu_helper_init(ctx, hs._h, B, P(d_nonces), P(d_pub), P(d_hin), P(d_lprep),
+                                     None, P(d_msgs) if s.prep_msg else None, P(d_hst),
+                                     hagg._h), "helper_init")
+        check(L.prio3gpu_prepare_next(ctx, ls._h, B, P(d_msgs) if s.prep_msg else None, P(d_lst),
+                                      None, None, lagg._h), "leader prepare_next")
+        if comm is not None:
+            comm.allreduce(vdaf, lagg)
+            comm.allreduce(vdaf, hagg)
+
+    for _ in range(args.warmup):
+        step()
+    check(L.prio3gpu_prof_enable(ctx, 1), "prof")
+    check(L.prio3gpu_prof_read(ctx, (ctypes.c_double * 16)(), (ctypes.c_uint64 * 16)(), 16), "prof")
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ms = (ctypes.c_double * 16)()
+    nl = (ctypes.c_uint64 * 16)()
+    nk = L.prio3gpu_prof_read(ctx, ms, nl, 16)
+    kt = {L.prio3gpu_prof_kernel_name(i).decode(): (ms[i], nl[i]) for i in range(nk) if nl[i]}
+    check(L.prio3gpu_prof_enable(ctx, 0), "prof")
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- parity gate: statuses, counts, aggregate == plaintext sum (and == CPU restatement) ------
+    assert int(d_lst.max().item()) == 0 and int(d_hst.max().item()) == 0, "rejected reports"
+    total_steps = args.warmup + args.steps
+    la, lc = lagg.read(0)
+    ha, hc = hagg.read(0)
+    exp_count = total_steps * B * world
+    assert lc == exp_count and hc == exp_count, (lc, hc, exp_count)
+    meas = gen["meas"]
+    if world == 1:
+        if kind == 2:
+            plain = [int(x) * tiles * total_steps for x in meas.sum(axis=0)]
+        elif kind == 3:
+            plain = [int((meas[:, 0] == i).sum()) * tiles * total_steps for i in range(length)]
+        else:
+            plain = int(meas[:, 0].sum()) * tiles * total_steps
+        assert vdaf.unshard([la, ha]) == plain, "aggregate != plaintext sum"
+    parity = "unshard(aggregate) == plaintext sum; status all ok"
+
+    reports = args.steps * B * world
+    value = reports / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- roofline of the dominant kernel (HIP events on the engine's stream) -------------------
+    perms = perms_per_report(args.config, s)
+    dom = max(kt.items(), key=lambda kv: kv[1][0])
+    dname, (dms, dlaunch) = dom
+    avg_launch_s = dms / 1e3 / dlaunch
+    # B reports per launch; k_jr runs once per aggregator (2 launches per step)
+    if dname in perms and perms[dname]:
+        ops = perms[dname] * B * OPS_PER_PERM
+        achieved = ops / avg_launch_s / 1e12
+        roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
+                "unit": "Tops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                "kernel": dname, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "model": f"{perms[dname]} Keccak-f[1600]/report x {OPS_PER_PERM} int32 ops "
+                         f"(SURVEY §8(d)) x {B} reports/launch"}
+    else:
+        roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1),
+                "unit": "Tops/s", "frac": None, "traffic": None, "kernel": dname,
+                "avg_launch_ms": round(avg_launch_s * 1e3, 3)}
+    prof_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+    if os.path.exists(prof_path):
+        try:
+            pm = json.load(open(prof_path))
+            roof["traffic"] = pm.get(dname, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+
+    # ---- CPU baseline: C restatement of prio 0.15.1, bounded sample, rank 0 at N = 1 -----------
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        done, t0 = 0, time.perf_counter()
+        while True:
+            res = ref.prepare_batch(gen["nonces"], gen["public"], gen["leader_in"],
+                                    gen["helper_in"], threads=nthr, outputs=False)
+            assert res["count"] == U
+            done += U
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        cpu_s = time.perf_counter() - t0
+        # cross-check the CPU restatement's aggregate with the GPU's (GPU = tiles*steps copies)
+        p = vdaf.modulus
+        mult = tiles * total_steps
+        gl = [(x * mult) % p for x in vdaf.decode_field_vec(res["agg_l"].tobytes())]
+        assert gl == vdaf.decode_field_vec(la), "GPU leader aggregate != CPU restatement"
+        cpu = {"value": round(done / cpu_s, 2), "unit": "reports/s", "cores": nthr,
+               "kind": "port",
+               "sample": f"{done} reports ({U} distinct, repeated) leader+helper prepare+aggregate, "
+                         f"{nthr} threads, {cpu_s:.1f} s; C restatement of prio 0.15.1 "
+                         f"(reference not buildable)"}
+
+    out = {
+        "metric": METRIC if args.config == "sumvec" else f"reports/sec prepared+aggregated, {label}",
+        "value": round(value, 2),
+        "unit": "reports/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u128 (Field128 mod p)" if s.field_size == 16 else "u64 (Field64 mod p)",
+        "data": f"synthetic: {U} distinct reports/rank (SURVEY §8(d) recipe) tiled x{tiles}, "
+                f"resident in HBM",
+        "config": {"workload": label, "reports_per_gpu_per_step": B,
+                   "parallelism": f"report-sharded x{world}, RCCL all-gather merge"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
+        "parity": parity,
+        "gen_seconds": round(gen_s, 1),
+    }
+    if cpu:
+        out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

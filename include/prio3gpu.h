@@ -162,6 +162,13 @@ int prio3gpu_comm_init(const uint8_t id[128], int nranks, int rank, int device,
 int prio3gpu_comm_destroy(prio3gpu_comm* comm);
 int prio3gpu_agg_allreduce(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg* agg);
 
+/* Per-kernel timing with HIP events on the context's stream (opt-in; bench.py uses it for the
+ * live roofline numbers).  prof_read returns the number of kernel ids and fills, per kernel id,
+ * the summed milliseconds and launch count since the last read. */
+int prio3gpu_prof_enable(prio3gpu_ctx* ctx, int on);
+int prio3gpu_prof_read(prio3gpu_ctx* ctx, double* ms, uint64_t* launches, int max_kernels);
+const char* prio3gpu_prof_kernel_name(int kernel_id);
+
 /* Device memory helpers (bench / tests that stage inputs in HBM without torch). */
 int prio3gpu_dev_alloc(prio3gpu_ctx* ctx, size_t bytes, void** out);
 int prio3gpu_dev_free(prio3gpu_ctx* ctx, void* p);

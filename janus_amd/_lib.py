@@ -68,6 +68,9 @@ def _declare(lib):
         "prio3gpu_comm_init": (c.c_int, [u8p, c.c_int, c.c_int, c.c_int, c.POINTER(P)]),
         "prio3gpu_comm_destroy": (c.c_int, [P]),
         "prio3gpu_agg_allreduce": (c.c_int, [P, P, P]),
+        "prio3gpu_prof_enable": (c.c_int, [P, c.c_int]),
+        "prio3gpu_prof_read": (c.c_int, [P, P, P, c.c_int]),
+        "prio3gpu_prof_kernel_name": (c.c_char_p, [c.c_int]),
         "prio3gpu_dev_alloc": (c.c_int, [P, c.c_size_t, c.POINTER(P)]),
         "prio3gpu_dev_free": (c.c_int, [P, P]),
         "prio3gpu_memcpy": (c.c_int, [P, P, P, c.c_size_t]),
@@ -88,7 +91,8 @@ EXPORTED = [
     "prio3gpu_agg_merge_bytes", "prio3gpu_prepare_init",
     "prio3gpu_prepare_shares_to_prepare_message", "prio3gpu_prepare_next", "prio3gpu_helper_init",
     "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
-    "prio3gpu_agg_allreduce", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
+    "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
+    "prio3gpu_prof_kernel_name", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
     "prio3gpu_last_error",
 ]
 

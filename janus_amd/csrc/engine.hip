@@ -125,6 +125,35 @@ struct DevBuf {
   uint8_t* u8() const { return static_cast<uint8_t*>(p); }
 };
 
+enum KernelId {
+  KID_QUERY = 0, KID_EXPAND, KID_JR, KID_FLP, KID_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_MERGE,
+  KID_OUT, KID_MERGE, KID_COUNT
+};
+const char* const kKernelNames[KID_COUNT] = {
+    "k_query_rand", "k_expand", "k_jr", "k_flp_query", "k_decide", "k_prepare_next",
+    "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge"};
+
+// Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
+struct Prof {
+  bool on = false;
+  struct Rec {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+};
+
 }  // namespace
 
 struct prio3gpu_ctx {
@@ -138,7 +167,30 @@ struct prio3gpu_ctx {
   DevBuf io[6];
   DevBuf perm, chunks, partials, pcounts;
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
+  Prof prof;
 };
+
+namespace {
+struct ProfScope {
+  prio3gpu_ctx* c;
+  int kid;
+  hipEvent_t a{}, b{};
+  ProfScope(prio3gpu_ctx* c_, int kid_) : c(c_), kid(kid_) {
+    if (c->prof.on) {
+      a = c->prof.get();
+      b = c->prof.get();
+      (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~ProfScope() {
+    if (c->prof.on) {
+      (void)hipEventRecord(b, c->stream);
+      c->prof.recs.push_back({kid, a, b});
+    }
+  }
+};
+}  // namespace
+#define PROF(kid) ProfScope prof_scope_##kid(c, kid)
 
 struct prio3gpu_state {
   prio3gpu_ctx* ctx = nullptr;
@@ -313,8 +365,11 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   CRows nonces{d_nonces, 16};
   CRows pub{d_pub, g.public_share_len};
   Rows t_rows{st->t.u8(), 16};
-  hipLaunchKernelGGL(k_query_rand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N, vk_lo, vk_hi,
-                     nonces, t_rows, d_status);
+  {
+    PROF(KID_QUERY);
+    hipLaunchKernelGGL(k_query_rand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N, vk_lo, vk_hi,
+                       nonces, t_rows, d_status);
+  }
   CRows meas, proof, blinds;
   if (st->agg_id == 0) {
     meas = CRows{d_in, g.leader_share_len};
@@ -323,16 +378,22 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   } else {
     Rows mo{st->meas.u8(), (size_t)g.meas_len * es};
     Rows po{st->proof.u8(), (size_t)g.proof_len * es};
-    hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
-                       (uint32_t)st->agg_id, CRows{d_in, g.helper_share_len}, mo, po, d_status);
+    {
+      PROF(KID_EXPAND);
+      hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
+                         (uint32_t)st->agg_id, CRows{d_in, g.helper_share_len}, mo, po, d_status);
+    }
     meas = CRows{mo.base, mo.stride};
     proof = CRows{po.base, po.stride};
     blinds = CRows{d_in + 32, g.helper_share_len};
   }
   if (g.jr_len > 0) {
-    hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
-                       (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
-                       Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status);
+    {
+      PROF(KID_JR);
+      hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
+                         (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
+                         Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status);
+    }
   }
   // FLP query: block per report
   FlpDims dims;
@@ -360,9 +421,12 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
     set_err("FLP LDS requirement %zu too large", lds);
     return PRIO3GPU_E_ARG;
   }
-  hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr), lds, c->stream, g, N, dims, meas, proof,
-                     CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                     CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status);
+  {
+    PROF(KID_FLP);
+    hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr), lds, c->stream, g, N, dims, meas, proof,
+                       CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status);
+  }
   HIPCHK(hipGetLastError());
   st->meas_rows = meas;
   st->n = n;
@@ -373,9 +437,12 @@ template <class FO>
 int launch_decide(prio3gpu_ctx* c, size_t n, const uint8_t* d_l, const uint8_t* d_h,
                   uint8_t* d_msg, uint8_t* d_status) {
   const Cfg& g = c->cfg;
-  hipLaunchKernelGGL(k_decide<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
-                     CRows{d_l, g.prep_share_len}, CRows{d_h, g.prep_share_len},
-                     Rows{d_msg, g.prep_msg_len ? g.prep_msg_len : 16}, d_status);
+  {
+    PROF(KID_DECIDE);
+    hipLaunchKernelGGL(k_decide<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
+                       CRows{d_l, g.prep_share_len}, CRows{d_h, g.prep_share_len},
+                       Rows{d_msg, g.prep_msg_len ? g.prep_msg_len : 16}, d_status);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -439,13 +506,19 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
   HIPCHK(hipMemcpyAsync(d_cb, cb.data(), (nch + 1) * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d_cs, cs.data(), nch * 4, hipMemcpyHostToDevice, c->stream));
   // The host vectors must outlive the async copies: synchronise before they can be reused.
-  hipLaunchKernelGGL(k_accum_partial<FO>, dim3(nch, tiles), dim3(256),
-                     256 * sizeof(typename FO::T), c->stream, g, st->meas_rows,
-                     reinterpret_cast<const uint32_t*>(c->perm.p), d_cb, d_status, epb,
-                     c->partials.u8(), reinterpret_cast<uint32_t*>(c->pcounts.p));
-  hipLaunchKernelGGL(k_accum_merge<FO>, grid1(g.out_len, 256), dim3(256), 0, c->stream, g, nch,
-                     d_cs, c->partials.u8(), reinterpret_cast<const uint32_t*>(c->pcounts.p),
-                     agg->share.u8(), reinterpret_cast<unsigned long long*>(agg->counts.p));
+  {
+    PROF(KID_ACC_PART);
+    hipLaunchKernelGGL(k_accum_partial<FO>, dim3(nch, tiles), dim3(256),
+                       256 * sizeof(typename FO::T), c->stream, g, st->meas_rows,
+                       reinterpret_cast<const uint32_t*>(c->perm.p), d_cb, d_status, epb,
+                       c->partials.u8(), reinterpret_cast<uint32_t*>(c->pcounts.p));
+  }
+  {
+    PROF(KID_ACC_MERGE);
+    hipLaunchKernelGGL(k_accum_merge<FO>, grid1(g.out_len, 256), dim3(256), 0, c->stream, g, nch,
+                       d_cs, c->partials.u8(), reinterpret_cast<const uint32_t*>(c->pcounts.p),
+                       agg->share.u8(), reinterpret_cast<unsigned long long*>(agg->counts.p));
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
@@ -456,8 +529,11 @@ int launch_out_shares(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8
                       uint8_t* d_out) {
   const Cfg& g = c->cfg;
   dim3 grid((g.out_len + 255) / 256, (unsigned)n);
-  hipLaunchKernelGGL(k_out_shares<FO>, grid, dim3(256), 0, c->stream, g, (uint32_t)n,
-                     st->meas_rows, Rows{d_out, (size_t)g.out_len * g.es}, d_status);
+  {
+    PROF(KID_OUT);
+    hipLaunchKernelGGL(k_out_shares<FO>, grid, dim3(256), 0, c->stream, g, (uint32_t)n,
+                       st->meas_rows, Rows{d_out, (size_t)g.out_len * g.es}, d_status);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -537,6 +613,11 @@ int prio3gpu_ctx_destroy(prio3gpu_ctx* c) {
   c->chunks.release();
   c->partials.release();
   c->pcounts.release();
+  for (auto& r : c->prof.recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto ev : c->prof.pool) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -664,9 +745,15 @@ int prio3gpu_agg_merge_bytes(prio3gpu_agg* a, uint32_t slot, const uint8_t* shar
   CHK(stage_in(c, c->io[0], share, bytes, &d_src));
   uint8_t* dst = a->share.u8() + slot * bytes;
   if (is_f64(c))
-    hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream, dst, d_src, nel);
+    {
+      PROF(KID_MERGE);
+      hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream, dst, d_src, nel);
+    }
   else
-    hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream, dst, d_src, nel);
+    {
+      PROF(KID_MERGE);
+      hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream, dst, d_src, nel);
+    }
   HIPCHK(hipGetLastError());
   uint64_t cur = 0;
   HIPCHK(hipMemcpyAsync(&cur, a->counts.u8() + (size_t)slot * 8, 8, hipMemcpyDeviceToHost, c->stream));
@@ -762,8 +849,11 @@ int prio3gpu_prepare_next(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const u
     }
     const uint8_t* d_msgs;
     CHK(stage_in(c, c->io[4], prep_msgs, n * 16, &d_msgs));
-    hipLaunchKernelGGL(k_prepare_next, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
-                       CRows{d_msgs, 16}, CRows{st->seed.u8(), 16}, d_status);
+    {
+      PROF(KID_PNEXT);
+      hipLaunchKernelGGL(k_prepare_next, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
+                         CRows{d_msgs, 16}, CRows{st->seed.u8(), 16}, d_status);
+    }
     HIPCHK(hipGetLastError());
   }
   if (out_output_shares) {
@@ -826,8 +916,11 @@ int prio3gpu_helper_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const ui
   else
     CHK(launch_decide<Field128Ops>(c, n, d_lps, st->prep.u8(), d_msg, d_status));
   if (g.jr_len) {
-    hipLaunchKernelGGL(k_prepare_next, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
-                       CRows{d_msg, 16}, CRows{st->seed.u8(), 16}, d_status);
+    {
+      PROF(KID_PNEXT);
+      hipLaunchKernelGGL(k_prepare_next, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
+                         CRows{d_msg, 16}, CRows{st->seed.u8(), 16}, d_status);
+    }
     HIPCHK(hipGetLastError());
   }
   if (agg) {
@@ -895,15 +988,58 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* a) 
   for (int r = 0; r < cm->nranks; ++r) {
     const uint8_t* src = cm->gather.u8() + (size_t)r * bytes;
     if (is_f64(c))
-      hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
-                         a->share.u8(), src, nel);
+      {
+        PROF(KID_MERGE);
+        hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
+                           a->share.u8(), src, nel);
+      }
     else
-      hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
-                         a->share.u8(), src, nel);
+      {
+        PROF(KID_MERGE);
+        hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
+                           a->share.u8(), src, nel);
+      }
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
+}
+
+int prio3gpu_prof_enable(prio3gpu_ctx* c, int on) {
+  if (!c) {
+    set_err("null context");
+    return PRIO3GPU_E_ARG;
+  }
+  c->prof.on = on != 0;
+  return 0;
+}
+
+int prio3gpu_prof_read(prio3gpu_ctx* c, double* ms, uint64_t* launches, int max_kernels) {
+  if (!c || !ms || !launches) {
+    set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < max_kernels; ++i) {
+    ms[i] = 0.0;
+    launches[i] = 0;
+  }
+  for (auto& r : c->prof.recs) {
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+    if (r.kid < max_kernels) {
+      ms[r.kid] += t;
+      launches[r.kid] += 1;
+    }
+    c->prof.pool.push_back(r.a);
+    c->prof.pool.push_back(r.b);
+  }
+  c->prof.recs.clear();
+  return KID_COUNT;
+}
+
+const char* prio3gpu_prof_kernel_name(int kid) {
+  return (kid >= 0 && kid < KID_COUNT) ? kKernelNames[kid] : "";
 }
 
 int prio3gpu_dev_alloc(prio3gpu_ctx* c, size_t bytes, void** out) {
