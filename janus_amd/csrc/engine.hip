@@ -478,11 +478,11 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
     std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
     for (size_t r = 0; r < n; ++r) perm[pos[sl ? sl[r] : 0]++] = (uint32_t)r;
   }
-  const uint32_t epb = std::min<uint32_t>(256, std::max<uint32_t>(1, g.out_len));
+  const uint32_t epb = std::min<uint32_t>(256, std::max<uint32_t>(1, g.meas_len));
   const uint32_t G = 256 / epb;
-  const uint32_t tiles = (g.out_len + epb - 1) / epb;
-  const size_t target_chunks = std::max<size_t>(1, 4096 / tiles);
-  size_t CH = std::max<size_t>(G, (n + target_chunks - 1) / target_chunks);
+  const uint32_t tiles = (g.meas_len + epb - 1) / epb;
+  const size_t target_chunks = std::max<size_t>(1, 2048 / tiles);
+  size_t CH = std::max<size_t>((size_t)G * 4, (n + target_chunks - 1) / target_chunks);
   auto& cb = c->h_chunk_begin;
   auto& cs = c->h_chunk_slot;
   cb.clear();
@@ -498,7 +498,7 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
   cb.push_back((uint32_t)n);
   CHK(c->perm.ensure(n * 4));
   CHK(c->chunks.ensure((size_t)(2 * nch + 1) * 4));
-  CHK(c->partials.ensure((size_t)nch * g.out_len * g.es));
+  CHK(c->partials.ensure((size_t)nch * g.meas_len * g.es));
   CHK(c->pcounts.ensure((size_t)nch * 4));
   HIPCHK(hipMemcpyAsync(c->perm.p, perm.data(), n * 4, hipMemcpyHostToDevice, c->stream));
   uint32_t* d_cb = reinterpret_cast<uint32_t*>(c->chunks.p);
@@ -509,13 +509,14 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
   {
     PROF(KID_ACC_PART);
     hipLaunchKernelGGL(k_accum_partial<FO>, dim3(nch, tiles), dim3(256),
-                       256 * sizeof(typename FO::T), c->stream, g, st->meas_rows,
+                       256 * sizeof(typename FO::T) + 16, c->stream, g, st->meas_rows,
                        reinterpret_cast<const uint32_t*>(c->perm.p), d_cb, d_status, epb,
                        c->partials.u8(), reinterpret_cast<uint32_t*>(c->pcounts.p));
   }
   {
     PROF(KID_ACC_MERGE);
-    hipLaunchKernelGGL(k_accum_merge<FO>, grid1(g.out_len, 256), dim3(256), 0, c->stream, g, nch,
+    const uint32_t bpe = (g.kind == KIND_SUMVEC || g.kind == KIND_SUM) ? g.bits : 1u;
+    hipLaunchKernelGGL(k_accum_merge<FO>, grid1(g.out_len, 256 / bpe), dim3(256), 0, c->stream, g, nch,
                        d_cs, c->partials.u8(), reinterpret_cast<const uint32_t*>(c->pcounts.p),
                        agg->share.u8(), reinterpret_cast<unsigned long long*>(agg->counts.p));
   }

@@ -1,4 +1,4 @@
-// Field64 / Field128 arithmetic for gfx950 (CDNA4), 32-bit-limb Montgomery built from
+// Field64 / Field128 arithmetic for gfx950 (CDNA4), Montgomery multiplication built from
 // v_mad_u64_u32 chains.  Replaces prio 0.15.1 `src/fp.rs` / `src/field.rs` (ext crate, called from
 // the Prio3 prepare path at aggregator/src/aggregator.rs:1777-1786).
 //
@@ -92,39 +92,44 @@ struct Field128Ops {
   static DEVI F128 neg(const F128& a) { return sub(zero(), a); }
   static DEVI F128 dbl(const F128& a) { return add(a, a); }
 
-  // Montgomery product a*b*2^-128 mod p (CIOS, 32-bit words).  Inputs < p, output < p.
+  // Montgomery product a*b*2^-128 mod p.  Inputs < p, output < p.
+  // 256-bit product from 16 v_mad_u64_u32 (four 64x64 products), then a 2-step, 64-bit-word REDC
+  // that needs no multiplier: p = 1 + (2^64 - 28) 2^64, so -p^-1 = -1 mod 2^64 (m = -t0) and
+  // m * p / 2^64 = [ -28m (low word), +m (next word) ] after the exact division.
   static DEVI F128 mul(const F128& a, const F128& b) {
-    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t bi = b.w[i];
-      uint64_t c;
-      c = (uint64_t)a.w[0] * bi + t0;              t0 = (uint32_t)c;
-      c = (uint64_t)a.w[1] * bi + t1 + (c >> 32);  t1 = (uint32_t)c;
-      c = (uint64_t)a.w[2] * bi + t2 + (c >> 32);  t2 = (uint32_t)c;
-      c = (uint64_t)a.w[3] * bi + t3 + (c >> 32);  t3 = (uint32_t)c;
-      c = (uint64_t)t4 + (c >> 32);
-      t4 = (uint32_t)c;
-      uint32_t t5 = (uint32_t)(c >> 32);
-      // reduction word m = -t0 ; t0 + m*P0 = t0 + m == 0 mod 2^32 with carry (t0 != 0)
-      const uint32_t m = 0u - t0;
-      c = (uint64_t)t1 + (t0 != 0u ? 1u : 0u);     t0 = (uint32_t)c;  // + m*P1 (=0)
-      c = (uint64_t)m * P2 + t2 + (c >> 32);       t1 = (uint32_t)c;
-      c = (uint64_t)m * P3 + t3 + (c >> 32);       t2 = (uint32_t)c;
-      c = (uint64_t)t4 + (c >> 32);                t3 = (uint32_t)c;
-      t4 = t5 + (uint32_t)(c >> 32);
-    }
-    // t < 2p: conditional subtract
-    F128 r{{t0, t1, t2, t3}};
-    if (t4 != 0u || !is_canonical(r)) {
-      // r - p mod 2^128  ==  r + c  mod 2^128
-      uint64_t c;
-      c = (uint64_t)t0 + 0xFFFFFFFFu;            r.w[0] = (uint32_t)c;
-      c = (uint64_t)t1 + 0xFFFFFFFFu + (c >> 32); r.w[1] = (uint32_t)c;
-      c = (uint64_t)t2 + 0x1Bu + (c >> 32);       r.w[2] = (uint32_t)c;
-      c = (uint64_t)t3 + (c >> 32);               r.w[3] = (uint32_t)c;
-    }
-    return r;
+    typedef unsigned __int128 u128;
+    const uint64_t alo = ((uint64_t)a.w[1] << 32) | a.w[0], ahi = ((uint64_t)a.w[3] << 32) | a.w[2];
+    const uint64_t blo = ((uint64_t)b.w[1] << 32) | b.w[0], bhi = ((uint64_t)b.w[3] << 32) | b.w[2];
+    const u128 p00 = (u128)alo * blo, p01 = (u128)alo * bhi, p10 = (u128)ahi * blo,
+               p11 = (u128)ahi * bhi;
+    const uint64_t t0 = (uint64_t)p00;
+    const u128 mid = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
+    const uint64_t t1 = (uint64_t)mid;
+    const u128 hi = (mid >> 64) + (p01 >> 64) + (p10 >> 64) + p11;
+    const uint64_t t2 = (uint64_t)hi, t3 = (uint64_t)(hi >> 64);
+    // REDC step 1
+    uint64_t m = 0 - t0;
+    u128 m28 = (u128)m * 28u;
+    u128 w0 = (u128)t1 + (uint64_t)(t0 != 0);
+    u128 x = (u128)t2 + m + ((u128)t3 << 64) + (w0 >> 64);
+    uint64_t w0lo = (uint64_t)w0;
+    uint64_t r0 = w0lo - (uint64_t)m28;
+    x = x - (m28 >> 64) - (uint64_t)(w0lo < (uint64_t)m28);
+    const uint64_t s0 = r0, s1 = (uint64_t)x, s2 = (uint64_t)(x >> 64);
+    // REDC step 2
+    m = 0 - s0;
+    m28 = (u128)m * 28u;
+    w0 = (u128)s1 + (uint64_t)(s0 != 0);
+    x = (u128)s2 + m + (w0 >> 64);
+    w0lo = (uint64_t)w0;
+    r0 = w0lo - (uint64_t)m28;
+    x = x - (m28 >> 64) - (uint64_t)(w0lo < (uint64_t)m28);
+    // result (x:r0) < 2p
+    u128 r = ((u128)(uint64_t)x << 64) | r0;
+    const u128 P = ((u128)0xFFFFFFFFFFFFFFE4ull << 64) | 1u;
+    if ((uint64_t)(x >> 64) != 0 || r >= P) r -= P;
+    const uint64_t lo = (uint64_t)r, hh = (uint64_t)(r >> 64);
+    return F128{{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hh, (uint32_t)(hh >> 32)}};
   }
   static DEVI F128 to_mont(const F128& a) { return mul(a, r2()); }
   static DEVI F128 from_mont(const F128& a) { return mul(a, one()); }

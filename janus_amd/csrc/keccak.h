@@ -14,7 +14,7 @@
 #define DEVI __device__ __forceinline__
 #endif
 
-__device__ __constant__ static const uint64_t kKeccakRC[24] = {
+constexpr uint64_t kRC[24] = {
     0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
     0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
     0x000000000000008aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000aull,
@@ -22,82 +22,116 @@ __device__ __constant__ static const uint64_t kKeccakRC[24] = {
     0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
     0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
 
-DEVI uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
+// 3-input bitwise ops (gfx950 v_bitop3_b32; LUT index = (src0<<2)|(src1<<1)|src2).
+DEVI uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+DEVI uint32_t chi3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0xD2); }  // a ^ (~b & c)
+// v_alignbit_b32: ((hi:lo) >> s)[31:0]
+DEVI uint32_t abit(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbit(hi, lo, s); }
 
-// One round on state a (indices x + 5y).
-#define KECCAK_ROUND(a, rc)                                                                     \
-  do {                                                                                          \
-    uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20];                                          \
-    uint64_t c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];                                          \
-    uint64_t c2 = a[2] ^ a[7] ^ a[12] ^ a[17] ^ a[22];                                          \
-    uint64_t c3 = a[3] ^ a[8] ^ a[13] ^ a[18] ^ a[23];                                          \
-    uint64_t c4 = a[4] ^ a[9] ^ a[14] ^ a[19] ^ a[24];                                          \
-    uint64_t d0 = c4 ^ rotl64(c1, 1);                                                           \
-    uint64_t d1 = c0 ^ rotl64(c2, 1);                                                           \
-    uint64_t d2 = c1 ^ rotl64(c3, 1);                                                           \
-    uint64_t d3 = c2 ^ rotl64(c4, 1);                                                           \
-    uint64_t d4 = c3 ^ rotl64(c0, 1);                                                           \
-    /* theta + rho + pi: b[y][2x+3y] = rot(a[x][y] ^ d[x], r[x][y]) ; b index = y + 5*(2x+3y) */ \
-    uint64_t b0 = a[0] ^ d0;                                                                    \
-    uint64_t b10 = rotl64(a[1] ^ d1, 1);                                                        \
-    uint64_t b20 = rotl64(a[2] ^ d2, 62);                                                       \
-    uint64_t b5 = rotl64(a[3] ^ d3, 28);                                                        \
-    uint64_t b15 = rotl64(a[4] ^ d4, 27);                                                       \
-    uint64_t b16 = rotl64(a[5] ^ d0, 36);                                                       \
-    uint64_t b1 = rotl64(a[6] ^ d1, 44);                                                        \
-    uint64_t b11 = rotl64(a[7] ^ d2, 6);                                                        \
-    uint64_t b21 = rotl64(a[8] ^ d3, 55);                                                       \
-    uint64_t b6 = rotl64(a[9] ^ d4, 20);                                                        \
-    uint64_t b7 = rotl64(a[10] ^ d0, 3);                                                        \
-    uint64_t b17 = rotl64(a[11] ^ d1, 10);                                                      \
-    uint64_t b2 = rotl64(a[12] ^ d2, 43);                                                       \
-    uint64_t b12 = rotl64(a[13] ^ d3, 25);                                                      \
-    uint64_t b22 = rotl64(a[14] ^ d4, 39);                                                      \
-    uint64_t b23 = rotl64(a[15] ^ d0, 41);                                                      \
-    uint64_t b8 = rotl64(a[16] ^ d1, 45);                                                       \
-    uint64_t b18 = rotl64(a[17] ^ d2, 15);                                                      \
-    uint64_t b3 = rotl64(a[18] ^ d3, 21);                                                       \
-    uint64_t b13 = rotl64(a[19] ^ d4, 8);                                                       \
-    uint64_t b14 = rotl64(a[20] ^ d0, 18);                                                      \
-    uint64_t b24 = rotl64(a[21] ^ d1, 2);                                                       \
-    uint64_t b9 = rotl64(a[22] ^ d2, 61);                                                       \
-    uint64_t b19 = rotl64(a[23] ^ d3, 56);                                                      \
-    uint64_t b4 = rotl64(a[24] ^ d4, 14);                                                       \
-    /* chi + iota */                                                                            \
-    a[0] = b0 ^ (~b1 & b2) ^ (rc);                                                              \
-    a[1] = b1 ^ (~b2 & b3);                                                                     \
-    a[2] = b2 ^ (~b3 & b4);                                                                     \
-    a[3] = b3 ^ (~b4 & b0);                                                                     \
-    a[4] = b4 ^ (~b0 & b1);                                                                     \
-    a[5] = b5 ^ (~b6 & b7);                                                                     \
-    a[6] = b6 ^ (~b7 & b8);                                                                     \
-    a[7] = b7 ^ (~b8 & b9);                                                                     \
-    a[8] = b8 ^ (~b9 & b5);                                                                     \
-    a[9] = b9 ^ (~b5 & b6);                                                                     \
-    a[10] = b10 ^ (~b11 & b12);                                                                 \
-    a[11] = b11 ^ (~b12 & b13);                                                                 \
-    a[12] = b12 ^ (~b13 & b14);                                                                 \
-    a[13] = b13 ^ (~b14 & b10);                                                                 \
-    a[14] = b14 ^ (~b10 & b11);                                                                 \
-    a[15] = b15 ^ (~b16 & b17);                                                                 \
-    a[16] = b16 ^ (~b17 & b18);                                                                 \
-    a[17] = b17 ^ (~b18 & b19);                                                                 \
-    a[18] = b18 ^ (~b19 & b15);                                                                 \
-    a[19] = b19 ^ (~b15 & b16);                                                                 \
-    a[20] = b20 ^ (~b21 & b22);                                                                 \
-    a[21] = b21 ^ (~b22 & b23);                                                                 \
-    a[22] = b22 ^ (~b23 & b24);                                                                 \
-    a[23] = b23 ^ (~b24 & b20);                                                                 \
-    a[24] = b24 ^ (~b20 & b21);                                                                 \
-  } while (0)
+// One Keccak round on a state split into 32-bit halves (l = low words, h = high words).
+//   theta: C[x] = xor of column (2 xor3 per half); lane ^= C[x-1] ^ rotl1(C[x+1]) (1 xor3 per half)
+//   rho:   rotl64 by r = 2 v_alignbit_b32 (swap when r = 32; none when r = 0)
+//   pi:    register renaming
+//   chi:   1 bitop3 per half;  iota: xor of the round constant halves
+// => 20 + 10 + 50 + 48 + 50 + 2 = 180 VALU ops per round.
+template <int R>
+DEVI void keccak_round32(uint32_t l[25], uint32_t h[25]) {
+  uint32_t cl[5], ch[5], rl[5], rh[5];
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {
+    cl[x] = xor3(xor3(l[x], l[x + 5], l[x + 10]), l[x + 15], l[x + 20]);
+    ch[x] = xor3(xor3(h[x], h[x + 5], h[x + 10]), h[x + 15], h[x + 20]);
+  }
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {  // rotl64(C[x], 1)
+    rl[x] = abit(cl[x], ch[x], 31);
+    rh[x] = abit(ch[x], cl[x], 31);
+  }
+  uint32_t bl[25], bh[25];
+
+  { const uint32_t tl = xor3(l[0], cl[4], rl[1]), th = xor3(h[0], ch[4], rh[1]);
+    bl[0] = tl; bh[0] = th; }
+  { const uint32_t tl = xor3(l[1], cl[0], rl[2]), th = xor3(h[1], ch[0], rh[2]);
+    bl[10] = abit(tl, th, 31); bh[10] = abit(th, tl, 31); }
+  { const uint32_t tl = xor3(l[2], cl[1], rl[3]), th = xor3(h[2], ch[1], rh[3]);
+    bl[20] = abit(th, tl, 2); bh[20] = abit(tl, th, 2); }
+  { const uint32_t tl = xor3(l[3], cl[2], rl[4]), th = xor3(h[3], ch[2], rh[4]);
+    bl[5] = abit(tl, th, 4); bh[5] = abit(th, tl, 4); }
+  { const uint32_t tl = xor3(l[4], cl[3], rl[0]), th = xor3(h[4], ch[3], rh[0]);
+    bl[15] = abit(tl, th, 5); bh[15] = abit(th, tl, 5); }
+  { const uint32_t tl = xor3(l[5], cl[4], rl[1]), th = xor3(h[5], ch[4], rh[1]);
+    bl[16] = abit(th, tl, 28); bh[16] = abit(tl, th, 28); }
+  { const uint32_t tl = xor3(l[6], cl[0], rl[2]), th = xor3(h[6], ch[0], rh[2]);
+    bl[1] = abit(th, tl, 20); bh[1] = abit(tl, th, 20); }
+  { const uint32_t tl = xor3(l[7], cl[1], rl[3]), th = xor3(h[7], ch[1], rh[3]);
+    bl[11] = abit(tl, th, 26); bh[11] = abit(th, tl, 26); }
+  { const uint32_t tl = xor3(l[8], cl[2], rl[4]), th = xor3(h[8], ch[2], rh[4]);
+    bl[21] = abit(th, tl, 9); bh[21] = abit(tl, th, 9); }
+  { const uint32_t tl = xor3(l[9], cl[3], rl[0]), th = xor3(h[9], ch[3], rh[0]);
+    bl[6] = abit(tl, th, 12); bh[6] = abit(th, tl, 12); }
+  { const uint32_t tl = xor3(l[10], cl[4], rl[1]), th = xor3(h[10], ch[4], rh[1]);
+    bl[7] = abit(tl, th, 29); bh[7] = abit(th, tl, 29); }
+  { const uint32_t tl = xor3(l[11], cl[0], rl[2]), th = xor3(h[11], ch[0], rh[2]);
+    bl[17] = abit(tl, th, 22); bh[17] = abit(th, tl, 22); }
+  { const uint32_t tl = xor3(l[12], cl[1], rl[3]), th = xor3(h[12], ch[1], rh[3]);
+    bl[2] = abit(th, tl, 21); bh[2] = abit(tl, th, 21); }
+  { const uint32_t tl = xor3(l[13], cl[2], rl[4]), th = xor3(h[13], ch[2], rh[4]);
+    bl[12] = abit(tl, th, 7); bh[12] = abit(th, tl, 7); }
+  { const uint32_t tl = xor3(l[14], cl[3], rl[0]), th = xor3(h[14], ch[3], rh[0]);
+    bl[22] = abit(th, tl, 25); bh[22] = abit(tl, th, 25); }
+  { const uint32_t tl = xor3(l[15], cl[4], rl[1]), th = xor3(h[15], ch[4], rh[1]);
+    bl[23] = abit(th, tl, 23); bh[23] = abit(tl, th, 23); }
+  { const uint32_t tl = xor3(l[16], cl[0], rl[2]), th = xor3(h[16], ch[0], rh[2]);
+    bl[8] = abit(th, tl, 19); bh[8] = abit(tl, th, 19); }
+  { const uint32_t tl = xor3(l[17], cl[1], rl[3]), th = xor3(h[17], ch[1], rh[3]);
+    bl[18] = abit(tl, th, 17); bh[18] = abit(th, tl, 17); }
+  { const uint32_t tl = xor3(l[18], cl[2], rl[4]), th = xor3(h[18], ch[2], rh[4]);
+    bl[3] = abit(tl, th, 11); bh[3] = abit(th, tl, 11); }
+  { const uint32_t tl = xor3(l[19], cl[3], rl[0]), th = xor3(h[19], ch[3], rh[0]);
+    bl[13] = abit(tl, th, 24); bh[13] = abit(th, tl, 24); }
+  { const uint32_t tl = xor3(l[20], cl[4], rl[1]), th = xor3(h[20], ch[4], rh[1]);
+    bl[14] = abit(tl, th, 14); bh[14] = abit(th, tl, 14); }
+  { const uint32_t tl = xor3(l[21], cl[0], rl[2]), th = xor3(h[21], ch[0], rh[2]);
+    bl[24] = abit(tl, th, 30); bh[24] = abit(th, tl, 30); }
+  { const uint32_t tl = xor3(l[22], cl[1], rl[3]), th = xor3(h[22], ch[1], rh[3]);
+    bl[9] = abit(th, tl, 3); bh[9] = abit(tl, th, 3); }
+  { const uint32_t tl = xor3(l[23], cl[2], rl[4]), th = xor3(h[23], ch[2], rh[4]);
+    bl[19] = abit(th, tl, 8); bh[19] = abit(tl, th, 8); }
+  { const uint32_t tl = xor3(l[24], cl[3], rl[0]), th = xor3(h[24], ch[3], rh[0]);
+    bl[4] = abit(tl, th, 18); bh[4] = abit(th, tl, 18); }
+#pragma unroll
+  for (int y = 0; y < 5; ++y) {
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      l[x + 5 * y] = chi3(bl[x + 5 * y], bl[(x + 1) % 5 + 5 * y], bl[(x + 2) % 5 + 5 * y]);
+      h[x + 5 * y] = chi3(bh[x + 5 * y], bh[(x + 1) % 5 + 5 * y], bh[(x + 2) % 5 + 5 * y]);
+    }
+  }
+  constexpr uint64_t rc = kRC[R];
+  if constexpr ((uint32_t)rc != 0u) l[0] ^= (uint32_t)rc;
+  if constexpr ((uint32_t)(rc >> 32) != 0u) h[0] ^= (uint32_t)(rc >> 32);
+}
+
+template <int R, int END>
+DEVI void keccak_rounds32(uint32_t l[25], uint32_t h[25]) {
+  if constexpr (R < END) {
+    keccak_round32<R>(l, h);
+    keccak_rounds32<R + 1, END>(l, h);
+  }
+}
 
 // Keccak-p[1600, NR]: the last NR rounds of Keccak-f (round constants RC[24-NR .. 23]).
 template <int NR = 24>
 DEVI void keccak_p(uint64_t a[25]) {
+  uint32_t l[25], h[25];
 #pragma unroll
-  for (int r = 24 - NR; r < 24; ++r) {
-    KECCAK_ROUND(a, kKeccakRC[r]);
+  for (int i = 0; i < 25; ++i) {
+    l[i] = (uint32_t)a[i];
+    h[i] = (uint32_t)(a[i] >> 32);
   }
+  keccak_rounds32<24 - NR, 24>(l, h);
+#pragma unroll
+  for (int i = 0; i < 25; ++i) a[i] = ((uint64_t)h[i] << 32) | l[i];
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -20,6 +20,7 @@
 #pragma once
 #include "field.h"
 #include "keccak.h"
+#include "wide.h"
 
 namespace p3g {
 
@@ -368,6 +369,23 @@ DEVI typename FO::T block_sum(typename FO::T x, typename FO::T* red, uint32_t ti
 //   f_{2j+1,k} = x_idx - 1/2      (-1/2 if padded) -> wire_2j+1 = L0 s_2j+1 + sum_k L_k x - 1/2 sum_k L_k
 // LDS layout (dynamic):  TP[2m] | NA[m] | NB[m] | LM[m] | MM[m] | RP[c+1] | PA[H*c] | PB[H*c] | RED[nthr] | flag
 // ------------------------------------------------------------------------------------------------
+// tab[i] = base^i (Montgomery) for i < n, by doubling: log2(n) block-wide rounds.  All threads call.
+template <class FO>
+DEVI void pow_table(typename FO::T* tab, typename FO::T base, uint32_t n, uint32_t tid,
+                    uint32_t nthr) {
+  if (tid == 0) {
+    tab[0] = FO::one_mont();
+    if (n > 1) tab[1] = base;
+  }
+  __syncthreads();
+  for (uint32_t s = 2; s < n; s <<= 1) {
+    const typename FO::T h = tab[s >> 1];
+    const typename FO::T bs = FO::mul(h, h);  // base^s
+    for (uint32_t i = tid; i < s && i + s < n; i += nthr) tab[i + s] = FO::mul(tab[i], bs);
+    __syncthreads();
+  }
+}
+
 struct FlpDims {
   uint32_t H;       // row groups in the main loop
   uint32_t cols;    // columns (chunk) for ParallelSum, 1 for Sum, 1 for Count
@@ -404,26 +422,17 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
 
   // ---- powers of t (Montgomery): TP[i] = t^i, i < 2m ----
   const T tm = FO::to_mont(FO::load(tq.at(r)));
-  if (tid == 0) {
-    TP[0] = FO::one_mont();
-    TP[1] = tm;
-  }
-  __syncthreads();
-  for (uint32_t s = 2; s < 2 * m; s <<= 1) {
-    const T base = TP[s >> 1];
-    const T b2 = FO::mul(base, base);  // t^s
-    for (uint32_t i = tid; i < s && i + s < 2 * m; i += nthr) TP[i + s] = FO::mul(TP[i], b2);
-    __syncthreads();
-  }
+  pow_table<FO>(TP, tm, 2 * m, tid, nthr);
   // ---- r powers ----
   T rm = FO::one_mont();
   if (cfg.jr_len > 0) rm = FO::to_mont(FO::load(jr.at(r)));
   if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
-    // RP[j] = r^(j+1), j < c ; MM[k] (k = 1..calls) = r^(c(k-1)) (stored temporarily)
-    for (uint32_t j = tid; j < c; j += nthr) RP[j] = mont_pow<FO>(rm, j + 1);
-    for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) MM[k] = mont_pow<FO>(rm, (uint64_t)c * (k - 1));
+    // RP[i] = r^i (i <= c);  MM[k] = (r^c)^(k-1) (k = 1..calls), multiplied by L_k below
+    pow_table<FO>(RP, rm, c + 1, tid, nthr);
+    const T rc = RP[c];
+    pow_table<FO>(MM + 1, rc, cfg.calls, tid, nthr);
   } else if (cfg.kind == KIND_SUM) {
-    for (uint32_t k = tid; k <= cfg.calls; k += nthr) RP[k] = mont_pow<FO>(rm, k);  // r^k
+    pow_table<FO>(RP, rm, cfg.calls + 1, tid, nthr);  // RP[k] = r^k
   }
   // ---- NTT inputs: NA <- t^(m-1-i) (bit-reversed), NB <- folded gadget poly (bit-reversed) ----
   bool bad = false;
@@ -478,15 +487,36 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
   if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
     for (uint32_t slot = tid; slot < H * c; slot += nthr) {
       const uint32_t j = slot % c, h = slot / c;
-      T accA = FO::zero(), accB = FO::zero();
-      for (uint32_t k = 1 + h; k <= cfg.calls; k += H) {
-        const uint32_t idx = (k - 1) * c + j;
-        if (idx < cfg.meas_len) {
-          const T x = FO::load(xr + (size_t)idx * ES);
-          bad |= !FO::is_canonical(x);
-          accA = FO::add(accA, FO::mul(MM[k], x));
-          accB = FO::add(accB, FO::mul(LM[k], x));
-          xsum = FO::add(xsum, x);
+      T accA, accB;
+      if constexpr (FO::ES == 16) {
+        // lazy reduction: raw 256-bit products summed, one Montgomery reduction per wire
+        Wide wa, wb;
+        wide_zero(wa);
+        wide_zero(wb);
+        for (uint32_t k = 1 + h; k <= cfg.calls; k += H) {
+          const uint32_t idx = (k - 1) * c + j;
+          if (idx < cfg.meas_len) {
+            const T x = FO::load(xr + (size_t)idx * ES);
+            bad |= !FO::is_canonical(x);
+            wide_mac(wa, MM[k], x);
+            wide_mac(wb, LM[k], x);
+            if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x);
+          }
+        }
+        accA = wide_reduce(wa);
+        accB = wide_reduce(wb);
+      } else {
+        accA = FO::zero();
+        accB = FO::zero();
+        for (uint32_t k = 1 + h; k <= cfg.calls; k += H) {
+          const uint32_t idx = (k - 1) * c + j;
+          if (idx < cfg.meas_len) {
+            const T x = FO::load(xr + (size_t)idx * ES);
+            bad |= !FO::is_canonical(x);
+            accA = FO::add(accA, FO::mul(MM[k], x));
+            accB = FO::add(accB, FO::mul(LM[k], x));
+            xsum = FO::add(xsum, x);
+          }
         }
       }
       PA[h * c + j] = accA;
@@ -504,7 +534,7 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
       const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
       const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
       bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
-      const T w0 = FO::add(FO::mul(l0, s0), FO::mul(RP[j], a));
+      const T w0 = FO::add(FO::mul(l0, s0), FO::mul(RP[j + 1], a));
       const T w1 = FO::sub(FO::add(FO::mul(l0, s1), b), half_l);
       FO::store(outp + (size_t)(1 + 2 * j) * ES, w0);
       FO::store(outp + (size_t)(2 + 2 * j) * ES, w1);
@@ -642,8 +672,12 @@ DEVI typename FO::T out_elem(const Cfg& cfg, const uint8_t* x, uint32_t e) {
   return FO::load(x + (size_t)e * FO::ES);
 }
 
-// Segmented partial sums.  chunk c covers perm[chunk_begin[c] .. chunk_begin[c+1]); all reports of
-// a chunk share one batch slot.  Block (chunk, elem-tile): EPB elements x G report groups.
+// Segmented partial sums of the raw MEASUREMENT-share elements.  truncate() is linear, so
+//   sum_r truncate(meas_r) = truncate(sum_r meas_r)
+// and the per-report truncation is applied once per chunk sum in k_accum_merge.  Thread e reads
+// element e of every report in its chunk: 16 B per lane, consecutive lanes consecutive elements
+// (fully coalesced).  chunk c covers perm[chunk_begin[c] .. chunk_begin[c+1]); all reports of a
+// chunk share one batch slot.  Block (chunk, tile): EPB elements x G report groups.
 template <class FO>
 __global__ void __launch_bounds__(256) k_accum_partial(Cfg cfg, CRows meas, const uint32_t* perm,
                                                        const uint32_t* chunk_begin,
@@ -659,36 +693,50 @@ __global__ void __launch_bounds__(256) k_accum_partial(Cfg cfg, CRows meas, cons
   const uint32_t e = blockIdx.y * epb + el;
   const uint32_t b0 = chunk_begin[ch], b1 = chunk_begin[ch + 1];
   T acc = FO::zero();
-  uint32_t cnt = 0;
-  if (g < G && e < cfg.out_len) {
-    for (uint32_t i = b0 + g; i < b1; i += G) {
+  if (g < G && e < cfg.meas_len) {
+    const size_t off = (size_t)e * FO::ES;
+    uint32_t i = b0 + g;
+    // 4 independent loads in flight per thread
+    for (; i + 3 * G < b1; i += 4 * G) {
+      const uint32_t r0 = perm[i], r1 = perm[i + G], r2 = perm[i + 2 * G], r3 = perm[i + 3 * G];
+      const T x0 = FO::load(meas.at(r0) + off), x1 = FO::load(meas.at(r1) + off);
+      const T x2 = FO::load(meas.at(r2) + off), x3 = FO::load(meas.at(r3) + off);
+      if (status[r0] == ST_OK) acc = FO::add(acc, x0);
+      if (status[r1] == ST_OK) acc = FO::add(acc, x1);
+      if (status[r2] == ST_OK) acc = FO::add(acc, x2);
+      if (status[r3] == ST_OK) acc = FO::add(acc, x3);
+    }
+    for (; i < b1; i += G) {
       const uint32_t r = perm[i];
-      if (status[r] != ST_OK) continue;
-      acc = FO::add(acc, out_elem<FO>(cfg, meas.at(r), e));
-      ++cnt;
+      const T x = FO::load(meas.at(r) + off);
+      if (status[r] == ST_OK) acc = FO::add(acc, x);
     }
   }
-  red[tid] = acc;
-  __syncthreads();
-  if (g == 0 && e < cfg.out_len) {
-    T s = acc;
-    for (uint32_t q = 1; q < G; ++q) s = FO::add(s, red[q * epb + el]);
-    FO::store(partials + ((size_t)ch * cfg.out_len + e) * FO::ES, s);
-  }
-  if (blockIdx.y == 0) {
-    // report count for this chunk (independent of element)
+  if (G > 1) {
+    red[tid] = acc;
     __syncthreads();
-    uint32_t* rc = reinterpret_cast<uint32_t*>(smem);
+    if (g == 0) {
+      for (uint32_t q = 1; q < G; ++q) acc = FO::add(acc, red[q * epb + el]);
+    }
+  }
+  if (g == 0 && e < cfg.meas_len)
+    FO::store(partials + ((size_t)ch * cfg.meas_len + e) * FO::ES, acc);
+  if (blockIdx.y == 0) {  // accepted-report count of this chunk (LDS word after `red`)
+    uint32_t* rc = reinterpret_cast<uint32_t*>(smem + 256 * sizeof(T));
     if (tid == 0) *rc = 0;
     __syncthreads();
-    if (el == 0 && cfg.out_len > 0) atomicAdd(rc, cnt);
+    uint32_t cnt = 0;
+    for (uint32_t i = b0 + tid; i < b1; i += blockDim.x) cnt += (status[perm[i]] == ST_OK);
+    if (cnt) atomicAdd(rc, cnt);
     __syncthreads();
     if (tid == 0) part_counts[ch] = *rc;
   }
 }
 
-// agg[slot(c)] += partial[c] for every chunk c, in chunk order (deterministic).  Chunks of one
-// slot are contiguous, so each thread keeps a register sum per slot run.
+// agg[slot(c)] += truncate(sum of partial[c]) for every slot run of chunks (chunks of one slot
+// are contiguous), in chunk order (deterministic).  Block = 256 threads over `bpe`-element groups
+// (bpe = bits for Sum/SumVec, 1 otherwise): each thread sums one measurement element over the run,
+// then one thread per output element applies truncate (sum_b 2^b x_b) and adds into agg.
 template <class FO>
 __global__ void __launch_bounds__(256) k_accum_merge(Cfg cfg, uint32_t nchunks,
                                                      const uint32_t* chunk_slot,
@@ -696,24 +744,37 @@ __global__ void __launch_bounds__(256) k_accum_merge(Cfg cfg, uint32_t nchunks,
                                                      const uint32_t* part_counts, uint8_t* agg,
                                                      unsigned long long* counts) {
   using T = typename FO::T;
-  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < cfg.out_len) {
-    uint32_t c = 0;
-    while (c < nchunks) {
-      const uint32_t slot = chunk_slot[c];
-      T acc = FO::zero();
-      uint32_t c1 = c;
-      while (c1 < nchunks && chunk_slot[c1] == slot) ++c1;
-#pragma unroll 8
+  __shared__ T sums[256];
+  const uint32_t bpe = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_SUM) ? cfg.bits : 1u;
+  const uint32_t opb = 256 / bpe;  // output elements per block
+  const uint32_t tid = threadIdx.x;
+  const uint32_t o = blockIdx.x * opb + tid / bpe, b = tid % bpe;
+  const bool act = (tid < opb * bpe) && o < cfg.out_len;
+  const uint32_t e = o * bpe + b;
+  uint32_t c = 0;
+  while (c < nchunks) {
+    const uint32_t slot = chunk_slot[c];
+    uint32_t c1 = c;
+    while (c1 < nchunks && chunk_slot[c1] == slot) ++c1;
+    T acc = FO::zero();
+    if (act) {
+#pragma unroll 4
       for (uint32_t q = c; q < c1; ++q)
-        acc = FO::add(acc, FO::load(partials + ((size_t)q * cfg.out_len + e) * FO::ES));
-      uint8_t* dst = agg + ((size_t)slot * cfg.out_len + e) * FO::ES;
-      FO::store(dst, FO::add(FO::load(dst), acc));
-      c = c1;
+        acc = FO::add(acc, FO::load(partials + ((size_t)q * cfg.meas_len + e) * FO::ES));
     }
+    sums[tid] = acc;
+    __syncthreads();
+    if (act && b == 0) {
+      T t = FO::zero();
+      for (int k = (int)bpe - 1; k >= 0; --k) t = FO::add(FO::dbl(t), sums[tid + k]);
+      uint8_t* dst = agg + ((size_t)slot * cfg.out_len + o) * FO::ES;
+      FO::store(dst, FO::add(FO::load(dst), t));
+    }
+    __syncthreads();
+    c = c1;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    for (uint32_t c = 0; c < nchunks; ++c) counts[chunk_slot[c]] += part_counts[c];
+  if (blockIdx.x == 0 && tid == 0) {
+    for (uint32_t q = 0; q < nchunks; ++q) counts[chunk_slot[q]] += part_counts[q];
   }
 }
 
