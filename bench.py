@@ -93,7 +93,7 @@ def main():
     from oracle.ref import Prio3Ref
 
     kind, bits, length, chunk, label = CONFIGS[args.config]
-    defaults = {"sumvec": (65536, 8192), "sum": (1 << 20, 16384), "histogram": (1 << 20, 16384),
+    defaults = {"sumvec": (262144, 8192), "sum": (1 << 20, 16384), "histogram": (1 << 20, 16384),
                 "count": (1 << 22, 65536)}
     B = args.reports or defaults[args.config][0]
     U = args.unique or defaults[args.config][1]
@@ -129,7 +129,10 @@ def main():
     torch.cuda.synchronize()
 
     ls, hs = vdaf.new_state(0, B), vdaf.new_state(1, B)
+    # running aggregates (the batch aggregation); with N > 1 each step accumulates into per-GPU
+    # partials that the RCCL merge flushes into the totals
     lagg, hagg = vdaf.new_aggregate(1), vdaf.new_aggregate(1)
+    lpart, hpart = (vdaf.new_aggregate(1), vdaf.new_aggregate(1)) if world > 1 else (lagg, hagg)
     comm = None
     if world > 1:
         uid = [Comm.unique_id() if rank == 0 else None]
@@ -147,12 +150,12 @@ def main():
                                       P(d_lst)), "leader prepare_init")
         check(L.prio3gpu_helper_init(ctx, hs._h, B, P(d_nonces), P(d_pub), P(d_hin), P(d_lprep),
                                      None, P(d_msgs) if s.prep_msg else None, P(d_hst),
-                                     hagg._h), "helper_init")
+                                     hpart._h), "helper_init")
         check(L.prio3gpu_prepare_next(ctx, ls._h, B, P(d_msgs) if s.prep_msg else None, P(d_lst),
-                                      None, None, lagg._h), "leader prepare_next")
-        if comm is not None:
-            comm.allreduce(vdaf, lagg)
-            comm.allreduce(vdaf, hagg)
+                                      None, None, lpart._h), "leader prepare_next")
+        if comm is not None:  # flush the per-GPU partials into the totals (RCCL + mod-p add)
+            comm.allreduce(vdaf, lpart, lagg)
+            comm.allreduce(vdaf, hpart, hagg)
 
     for _ in range(args.warmup):
         step()
@@ -189,14 +192,17 @@ def main():
     exp_count = total_steps * B * world
     assert lc == exp_count and hc == exp_count, (lc, hc, exp_count)
     meas = gen["meas"]
-    if world == 1:
-        if kind == 2:
-            plain = [int(x) * tiles * total_steps for x in meas.sum(axis=0)]
-        elif kind == 3:
-            plain = [int((meas[:, 0] == i).sum()) * tiles * total_steps for i in range(length)]
-        else:
-            plain = int(meas[:, 0].sum()) * tiles * total_steps
-        assert vdaf.unshard([la, ha]) == plain, "aggregate != plaintext sum"
+    if kind == 2:
+        plain = [int(x) * tiles * total_steps for x in meas.sum(axis=0)]
+    elif kind == 3:
+        plain = [int((meas[:, 0] == i).sum()) * tiles * total_steps for i in range(length)]
+    else:
+        plain = int(meas[:, 0].sum()) * tiles * total_steps
+    if dist is not None:  # every rank holds the merged totals: compare with all ranks' plaintext
+        allp = [None] * world
+        dist.all_gather_object(allp, plain)
+        plain = [sum(col) for col in zip(*allp)] if isinstance(plain, list) else sum(allp)
+    assert vdaf.unshard([la, ha]) == plain, "aggregate != plaintext sum"
     parity = "unshard(aggregate) == plaintext sum; status all ok"
 
     reports = args.steps * B * world

@@ -155,12 +155,16 @@ int prio3gpu_helper_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const 
 
 /* Multi-GPU merge of per-GPU partial aggregates (one process per GPU).  RCCL all-gather of the
  * raw field-element bytes over xGMI, then a mod-p add kernel (RCCL sum is neither modular nor
- * 128-bit).  Counts are summed with an RCCL uint64 all-reduce. */
+ * 128-bit).  Counts are summed with an RCCL uint64 all-reduce.
+ * agg_allreduce: total += sum over ranks of local, then local is reset (the per-GPU partial of one
+ * aggregation job is flushed into the running aggregate, like Accumulator::flush_to_datastore,
+ * accumulator.rs:133-215).  With total == NULL, local is replaced by the sum over ranks. */
 int prio3gpu_comm_unique_id(uint8_t out_id[128]);
 int prio3gpu_comm_init(const uint8_t id[128], int nranks, int rank, int device,
                        prio3gpu_comm** out);
 int prio3gpu_comm_destroy(prio3gpu_comm* comm);
-int prio3gpu_agg_allreduce(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg* agg);
+int prio3gpu_agg_allreduce(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg* local,
+                           prio3gpu_agg* total);
 
 /* Per-kernel timing with HIP events on the context's stream (opt-in; bench.py uses it for the
  * live roofline numbers).  prof_read returns the number of kernel ids and fills, per kernel id,

@@ -67,7 +67,7 @@ def _declare(lib):
         "prio3gpu_comm_unique_id": (c.c_int, [u8p]),
         "prio3gpu_comm_init": (c.c_int, [u8p, c.c_int, c.c_int, c.c_int, c.POINTER(P)]),
         "prio3gpu_comm_destroy": (c.c_int, [P]),
-        "prio3gpu_agg_allreduce": (c.c_int, [P, P, P]),
+        "prio3gpu_agg_allreduce": (c.c_int, [P, P, P, P]),
         "prio3gpu_prof_enable": (c.c_int, [P, c.c_int]),
         "prio3gpu_prof_read": (c.c_int, [P, P, P, c.c_int]),
         "prio3gpu_prof_kernel_name": (c.c_char_p, [c.c_int]),

@@ -972,36 +972,52 @@ int prio3gpu_comm_destroy(prio3gpu_comm* cm) {
   return 0;
 }
 
-int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* a) {
-  if (!cm || !c || !a || a->ctx != c) {
+int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* local,
+                           prio3gpu_agg* total) {
+  if (!cm || !c || !local || local->ctx != c || (total && (total->ctx != c ||
+                                                           total->slots != local->slots))) {
     set_err("bad argument");
     return PRIO3GPU_E_ARG;
   }
   HIPCHK(hipSetDevice(c->device));
-  const size_t nel = (size_t)a->slots * c->cfg.out_len;
+  const size_t nel = (size_t)local->slots * c->cfg.out_len;
   const size_t bytes = nel * c->cfg.es;
   CHK(cm->gather.ensure(bytes * cm->nranks));
-  // all-gather raw LE field-element bytes, then sum every rank's share (rank order) mod p
-  RCCLCHK(ncclAllGather(a->share.p, cm->gather.p, bytes, ncclUint8, cm->comm, c->stream));
-  RCCLCHK(ncclAllReduce(a->counts.p, a->counts.p, a->slots, ncclUint64, ncclSum, cm->comm,
+  CHK(cm->cgather.ensure((size_t)local->slots * 8));
+  // all-gather the raw LE field-element bytes; counts: uint64 sum
+  RCCLCHK(ncclAllGather(local->share.p, cm->gather.p, bytes, ncclUint8, cm->comm, c->stream));
+  RCCLCHK(ncclAllReduce(local->counts.p, cm->cgather.p, local->slots, ncclUint64, ncclSum, cm->comm,
                         c->stream));
-  HIPCHK(hipMemsetAsync(a->share.p, 0, bytes, c->stream));
+  prio3gpu_agg* dst = total ? total : local;
+  if (!total) HIPCHK(hipMemsetAsync(local->share.p, 0, bytes, c->stream));
+  // dst += sum over ranks, in rank order (identical on every rank; mod-p addition is exact)
   for (int r = 0; r < cm->nranks; ++r) {
     const uint8_t* src = cm->gather.u8() + (size_t)r * bytes;
-    if (is_f64(c))
-      {
-        PROF(KID_MERGE);
+    {
+      PROF(KID_MERGE);
+      if (is_f64(c))
         hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
-                           a->share.u8(), src, nel);
-      }
-    else
-      {
-        PROF(KID_MERGE);
+                           dst->share.u8(), src, nel);
+      else
         hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
-                           a->share.u8(), src, nel);
-      }
+                           dst->share.u8(), src, nel);
+    }
   }
   HIPCHK(hipGetLastError());
+  // counts
+  std::vector<unsigned long long> sum(local->slots), cur(local->slots);
+  HIPCHK(hipMemcpyAsync(sum.data(), cm->cgather.p, local->slots * 8, hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(cur.data(), dst->counts.p, local->slots * 8, hipMemcpyDeviceToHost,
+                        c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (uint32_t s = 0; s < local->slots; ++s) cur[s] = (total ? cur[s] : 0ull) + sum[s];
+  HIPCHK(hipMemcpyAsync(dst->counts.p, cur.data(), local->slots * 8, hipMemcpyHostToDevice,
+                        c->stream));
+  if (total) {  // the local partial has been merged: reset it for the next job
+    HIPCHK(hipMemsetAsync(local->share.p, 0, bytes, c->stream));
+    HIPCHK(hipMemsetAsync(local->counts.p, 0, (size_t)local->slots * 8, c->stream));
+  }
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }

@@ -305,8 +305,13 @@ class Comm:
         check(lib().prio3gpu_comm_unique_id(_ptr(buf)), "comm_unique_id")
         return buf.tobytes()
 
-    def allreduce(self, vdaf: Prio3Gpu, agg: AggregateShares):
-        check(lib().prio3gpu_agg_allreduce(self._h, vdaf._ctx, agg._h), "agg_allreduce")
+    def allreduce(self, vdaf: Prio3Gpu, local: AggregateShares,
+                  total: Optional[AggregateShares] = None):
+        """total += sum over ranks of `local` (then `local` is reset); without `total`, `local`
+        becomes the sum over ranks."""
+        check(lib().prio3gpu_agg_allreduce(self._h, vdaf._ctx, local._h,
+                                           total._h if total is not None else None),
+              "agg_allreduce")
 
     def close(self):
         if getattr(self, "_h", None):

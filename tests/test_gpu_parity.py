@@ -205,3 +205,21 @@ def test_agg_merge_bytes():
     got, cnt = agg.read(1)
     x = v.decode_field_vec(exp)
     assert v.decode_field_vec(got) == [(2 * a) % v.modulus for a in x] and cnt == 10
+
+
+def test_rccl_merge_single_rank():
+    """RCCL all-gather + mod-p merge path with one rank: total += local, local reset."""
+    from janus_amd.prio3 import Comm
+    b = batch("hist4")
+    v = gpu_vdaf(b)
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    ls = v.new_state(0, b.n)
+    _, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    local, total = v.new_aggregate(1), v.new_aggregate(1)
+    v.prepare_next(ls, b.prep_msg, lst, want_output_shares=False, agg=local)
+    comm.allreduce(v, local, total)
+    comm.allreduce(v, local, total)  # local was reset: no double counting
+    got, cnt = total.read(0)
+    assert got == expected_aggregate(b, "leader")[0] and cnt == b.n
+    assert local.read(0)[1] == 0
+    comm.close()
