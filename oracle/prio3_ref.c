@@ -878,3 +878,12 @@ long long p3ref_prepare_batch(const p3ref* r, size_t n, int threads, const u8* n
   free(jobs);
   return count;
 }
+
+/* SHAKE128 one-shot (tests cross-check against hashlib / FIPS 202). */
+void p3ref_shake128(const u8* msg, size_t len, u8* out, size_t outlen) {
+  shake h;
+  shake_init(&h);
+  shake_absorb(&h, msg, len);
+  shake_finish(&h);
+  shake_squeeze(&h, out, outlen);
+}

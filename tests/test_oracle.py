@@ -1,0 +1,125 @@
+"""CPU checks of the oracle (test infrastructure): SHAKE128 against FIPS 202 / hashlib, field
+constants, the committed golden transcripts, the C restatement against the Python restatement,
+and the end-to-end property unshard(aggregate) == plaintext sum
+(integration_tests/tests/common/mod.rs:225-398)."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import prio3 as O
+from tests.reports import CONFIGS, make_batch, plaintext_sum
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "prio3_transcripts.json")))
+
+
+def test_shake128_fips202_kat():
+    # FIPS 202 / NIST example: SHAKE128("") first 16 bytes
+    assert hashlib.shake_128(b"").hexdigest(16) == "7f9c2ba4e88f827d616045507605853e"
+    x = O.XofShake128(bytes(16), O.domain_separation_tag(2, 1), b"\x01")
+    assert x.stream(32) == hashlib.shake_128(b"\x08" + O.domain_separation_tag(2, 1) +
+                                             bytes(16) + b"\x01").digest(32)
+
+
+def test_c_keccak_matches_hashlib():
+    from oracle.ref import lib
+    l = lib()
+    l.p3ref_shake128.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    rng = np.random.default_rng(1)
+    for n in [0, 1, 167, 168, 169, 336, 1000]:
+        msg = rng.integers(0, 256, n, dtype=np.uint8)
+        out = np.zeros(500, np.uint8)
+        l.p3ref_shake128(msg.ctypes.data, n, out.ctypes.data, 500)
+        assert out.tobytes() == hashlib.shake_128(msg.tobytes()).digest(500)
+
+
+def test_field_constants():
+    for F, k in ((O.Field64, 32), (O.Field128, 66)):
+        p = F.MODULUS
+        assert (p - 1) % (1 << k) == 0
+        g = F.GEN
+        assert pow(g, 1 << k, p) == 1 and pow(g, 1 << (k - 1), p) != 1
+    assert O.Field64.MODULUS == 18446744069414584321
+    assert O.Field128.MODULUS == 340282366920938462946865773367900766209
+    assert O.Field64.GEN == 1753635133440165772
+    assert O.Field128.GEN == 145091266659756586618791329697897684742
+
+
+def test_domain_separation_tag():
+    # [VERSION=7, class=0, algo id u32 BE, usage u16 BE]
+    assert O.domain_separation_tag(0x00000002, 7) == bytes([7, 0, 0, 0, 0, 2, 0, 7])
+
+
+def _enc(b):
+    if len(b) > 4096:
+        return {"sha256": hashlib.sha256(b).hexdigest(), "len": len(b)}
+    return b.hex()
+
+
+@pytest.mark.parametrize("cfg", GOLD["configs"], ids=[c["name"] for c in GOLD["configs"]])
+def test_oracle_reproduces_golden(cfg):
+    v = CONFIGS[cfg["name"]]["ctor"]()
+    vk = bytes.fromhex(cfg["verify_key"])
+    if cfg["name"] == "sumvec_8_1000":
+        pass  # one report, ~0.5 s
+    lo, ho = [], []
+    for rep in cfg["reports"]:
+        t = O.run_vdaf(v, vk, bytes.fromhex(rep["nonce"]), rep["measurement"],
+                       bytes.fromhex(rep["rand"]))
+        for k, val in t.items():
+            assert _enc(val) == rep[k], (cfg["name"], k)
+        lo.append(v.fld.decode_vec(t["leader_out_share"]))
+        ho.append(v.fld.decode_vec(t["helper_out_share"]))
+    assert _enc(v.fld.encode_vec(v.aggregate(lo))) == cfg["leader_agg_share"]
+    assert v.unshard([v.aggregate(lo), v.aggregate(ho)]) == cfg["unsharded"]
+
+
+@pytest.mark.parametrize("name", ["count", "sum8", "sum32", "sumvec_small", "countvec15", "hist4",
+                                  "hist256"])
+def test_c_restatement_matches_python(name):
+    from oracle.ref import Prio3Ref
+    b = make_batch(name, 5)
+    c = CONFIGS[name]
+    r = Prio3Ref(c["kind"], b.verify_key, c["bits"], c["length"], c["chunk"])
+    g = r.gen(name.encode(), 0, 5, threads=2)
+    for k in ["nonces", "public", "leader_in", "helper_in"]:
+        np.testing.assert_array_equal(g[k], getattr(b, k))
+    res = r.prepare_batch(b.nonces, b.public, b.leader_in, b.helper_in, threads=2)
+    np.testing.assert_array_equal(res["lprep"], b.leader_prep)
+    np.testing.assert_array_equal(res["hprep"], b.helper_prep)
+    np.testing.assert_array_equal(res["msgs"], b.prep_msg)
+    assert (res["status"] == 0).all() and res["count"] == 5
+
+
+@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_small", "hist4"])
+def test_unshard_equals_plaintext(name):
+    b = make_batch(name, 12)
+    v = b.vdaf
+    la = v.aggregate([v.fld.decode_vec(x.tobytes()) for x in b.leader_out])
+    ha = v.aggregate([v.fld.decode_vec(x.tobytes()) for x in b.helper_out])
+    assert v.unshard([la, ha]) == plaintext_sum(b)
+
+
+def test_tampered_share_rejected_by_oracle():
+    b = make_batch("sumvec_small", 1)
+    v = b.vdaf
+    share = v.decode_input_share(0, b.leader_in[0].tobytes())
+    share.meas_share[0] = (share.meas_share[0] + 1) % v.fld.MODULUS
+    pub = v.decode_public_share(b.public[0].tobytes())
+    nonce = b.nonces[0].tobytes()
+    _, lps = v.prepare_init(b.verify_key, 0, nonce, pub, share)
+    _, hps = v.prepare_init(b.verify_key, 1, nonce, pub,
+                            v.decode_input_share(1, b.helper_in[0].tobytes()))
+    with pytest.raises(ValueError):
+        v.prep_shares_to_prep([lps, hps])
+
+
+def test_noncanonical_decode_rejected():
+    b = make_batch("hist4", 1)
+    raw = bytearray(b.leader_in[0].tobytes())
+    raw[:16] = b"\xff" * 16
+    with pytest.raises(ValueError):
+        b.vdaf.decode_input_share(0, bytes(raw))
