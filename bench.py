@@ -227,11 +227,20 @@ def main():
         roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": None, "traffic": None, "kernel": dname,
                 "avg_launch_ms": round(avg_launch_s * 1e3, 3)}
+    if dname in perms and perms[dname]:
+        perm_rate = perms[dname] * B / avg_launch_s
+        roof["keccak_perms_per_s"] = round(perm_rate, 1)
+        roof["algorithmic_hbm_bytes_per_launch"] = (
+            B * s.meas_len * s.field_size if dname == "k_jr" else
+            B * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand" else None)
     prof_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(prof_path):
+    if os.path.exists(prof_path):  # PMC pass of the same command (tools/profile_round.sh)
         try:
-            pm = json.load(open(prof_path))
-            roof["traffic"] = pm.get(dname, {}).get("hbm_bytes_per_launch")
+            pm = json.load(open(prof_path)).get(dname, {})
+            roof["traffic"] = pm.get("hbm_bytes_per_launch")
+            if pm.get("SQ_INSTS_VALU") and dname in perms and perms[dname]:
+                # instructions per lane-report: per-wave count / reports per wave (64)
+                roof["valu_insts_per_perm"] = round(pm["valu_insts_per_wave"] / perms[dname], 1)
         except Exception:
             pass
 

@@ -14,5 +14,5 @@ timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -
 timeout -k 10 500 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/sq" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-baseline 0 > "$O/sq.log" 2>&1
 python3 "$R/tools/pmc_summary.py" --trace "$O/trace" --fetch "$O/fetch" --write "$O/write" --sq "$O/sq" --out "$R/gpurun_out/pmc_sumvec_$TAG.json" > "$O/summary.txt"
 cp "$O"/trace/*kernel_stats.csv "$R/gpurun_out/kernel_stats_$TAG.csv" 2>/dev/null || find "$O/trace" -name "*kernel_stats.csv" -exec cp {} "$R/gpurun_out/kernel_stats_$TAG.csv" \;
-tail -1 "$O/trace.log" > "$R/gpurun_out/bench_under_rocprof_$TAG.json"
+grep "^{\"metric\"" "$O/trace.log" > "$R/gpurun_out/bench_under_rocprof_$TAG.json" || true
 cat "$O/summary.txt"
