@@ -415,7 +415,7 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
     nthr = (g.kind == KIND_SUM) ? 64 : 64;
   }
   const size_t esz = sizeof(typename FO::T);
-  size_t lds = esz * (6 * (size_t)g.m + dims.rp_len + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
+  size_t lds = esz * (6 * (size_t)g.m + dims.rp_len + 2 * (size_t)dims.H * dims.cols + nthr + 128) + 16;
   lds = (lds + 15) & ~(size_t)15;
   if (lds > 160 * 1024) {
     set_err("FLP LDS requirement %zu too large", lds);

@@ -69,39 +69,45 @@ DEVI void st64(uint8_t* p, uint64_t v) { *reinterpret_cast<uint64_t*>(p) = v; }
 template <class FO, int NR>
 DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out);
 
+// One permutation per loop iteration (a single inlined Keccak-f per loop: ~35 KB of VOP3 code, so
+// two hot copies would not fit the instruction cache).  168-byte blocks alternate parity: even
+// blocks hold 10 whole elements + the low half of the next, odd blocks start with its high half.
 template <>
 DEVI void squeeze_vec<Field128Ops, 24>(uint64_t s[25], uint32_t n, uint8_t* out) {
   using FO = Field128Ops;
   uint32_t cnt = 0;
+  uint32_t parity = 0;
+  uint64_t carry = 0;
   while (true) {
-    // block A: elements (s0,s1)..(s18,s19); s20 = low half of the element straddling blocks
+    if (parity == 0) {
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
-      if (cnt < n && FO::is_canonical(e)) {
-        FO::store(out + (size_t)cnt * 16, e);
-        ++cnt;
+      for (int k = 0; k < 10; ++k) {
+        F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
+        if (cnt < n && FO::is_canonical(e)) {
+          FO::store(out + (size_t)cnt * 16, e);
+          ++cnt;
+        }
+      }
+      carry = s[20];
+    } else {
+      {
+        F128 e = FO::from_u64x2(carry, s[0]);
+        if (cnt < n && FO::is_canonical(e)) {
+          FO::store(out + (size_t)cnt * 16, e);
+          ++cnt;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
+        if (cnt < n && FO::is_canonical(e)) {
+          FO::store(out + (size_t)cnt * 16, e);
+          ++cnt;
+        }
       }
     }
     if (cnt >= n) break;
-    const uint64_t carry = s[20];
-    keccak_p<24>(s);
-    {
-      F128 e = FO::from_u64x2(carry, s[0]);
-      if (cnt < n && FO::is_canonical(e)) {
-        FO::store(out + (size_t)cnt * 16, e);
-        ++cnt;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
-      if (cnt < n && FO::is_canonical(e)) {
-        FO::store(out + (size_t)cnt * 16, e);
-        ++cnt;
-      }
-    }
-    if (cnt >= n) break;
+    parity ^= 1u;
     keccak_p<24>(s);
   }
 }
@@ -185,20 +191,12 @@ DEVI void jr_part(uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t
   const int64_t padw = total >> 3;              // word holding the 0x1F pad byte
   const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
   uint64_t s[25];
-  // block 0 (prefix + first data words)
 #pragma unroll
-  for (int w = 0; w < 21; ++w) {
-    uint64_t v = (w < 5) ? pre.w[w] : jr_data_word(w, data, nd, nonce_hi);
-    if (padw == w) v ^= padv;
-    if (nblocks == 1 && w == 20) v ^= 0x8000000000000000ull;
-    s[w] = v;
-  }
-#pragma unroll
-  for (int i = 21; i < 25; ++i) s[i] = 0ull;
-  keccak_p<24>(s);
-  for (int64_t b = 1; b < nblocks; ++b) {
-    // fast path: every word of the block is data:  D index 21b+20-5 < nd  and no padding inside
-    const bool fast = (21 * b + 15 < nd) && (21 * b + 20 < padw);
+  for (int i = 0; i < 25; ++i) s[i] = 0ull;
+  // One permutation per iteration (single inlined Keccak-f, see squeeze_vec).  Block 0 carries the
+  // 42-byte prefix; "fast" blocks are pure data (the common case); the last block(s) are padded.
+  for (int64_t b = 0; b < nblocks; ++b) {
+    const bool fast = (b >= 1) && (21 * b + 15 < nd) && (21 * b + 20 < padw);
     if (fast) {
       const uint64_t* D = reinterpret_cast<const uint64_t*>(data) + (21 * b - 6);
       uint64_t prev = D[0];
@@ -207,6 +205,14 @@ DEVI void jr_part(uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t
         const uint64_t cur = D[w + 1];
         s[w] ^= (prev >> 48) | (cur << 16);
         prev = cur;
+      }
+    } else if (b == 0) {
+#pragma unroll
+      for (int w = 0; w < 21; ++w) {
+        uint64_t v = (w < 5) ? pre.w[w] : jr_data_word(w, data, nd, nonce_hi);
+        if (padw == w) v ^= padv;
+        if (nblocks == 1 && w == 20) v ^= 0x8000000000000000ull;
+        s[w] ^= v;
       }
     } else {
 #pragma unroll
@@ -369,21 +375,83 @@ DEVI typename FO::T block_sum(typename FO::T x, typename FO::T* red, uint32_t ti
 //   f_{2j+1,k} = x_idx - 1/2      (-1/2 if padded) -> wire_2j+1 = L0 s_2j+1 + sum_k L_k x - 1/2 sum_k L_k
 // LDS layout (dynamic):  TP[2m] | NA[m] | NB[m] | LM[m] | MM[m] | RP[c+1] | PA[H*c] | PB[H*c] | RED[nthr] | flag
 // ------------------------------------------------------------------------------------------------
-// tab[i] = base^i (Montgomery) for i < n, by doubling: log2(n) block-wide rounds.  All threads call.
+// Wave-level inclusive product scan (6 shuffle steps): lane l returns base^(l+1).
 template <class FO>
-DEVI void pow_table(typename FO::T* tab, typename FO::T base, uint32_t n, uint32_t tid,
-                    uint32_t nthr) {
-  if (tid == 0) {
-    tab[0] = FO::one_mont();
-    if (n > 1) tab[1] = base;
+DEVI typename FO::T wave_pow_scan(typename FO::T base, uint32_t lane) {
+  typename FO::T v = base;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    typename FO::T y;
+#pragma unroll
+    for (int w = 0; w < FO::NW; ++w) y.w[w] = __shfl_up(v.w[w], off, 64);
+    if (lane >= (uint32_t)off) v = FO::mul(v, y);
+  }
+  return v;
+}
+
+// tab[i] = base^i (Montgomery) for i < n (n <= 4096), built by ONE wave with two product scans:
+// base^1..base^64 by lanes, giant steps (base^64)^q by lanes, then tab[64q + l] = base^(64q) base^l.
+// No barriers inside (the caller synchronises).
+template <class FO>
+DEVI void wave_pow_table(typename FO::T* tab, typename FO::T base, uint32_t n, uint32_t lane) {
+  using T = typename FO::T;
+  const T v = wave_pow_scan<FO>(base, lane);  // base^(lane+1)
+  if (lane == 0) tab[0] = FO::one_mont();
+  if (lane + 1 < n) tab[lane + 1] = v;
+  const uint32_t nq = (n + 63) >> 6;
+  if (nq > 1) {
+    T b64, bl;
+#pragma unroll
+    for (int w = 0; w < FO::NW; ++w) {
+      b64.w[w] = __shfl(v.w[w], 63, 64);
+      bl.w[w] = __shfl(v.w[w], (int)((lane + 63) & 63), 64);  // base^lane (lane 0: fixed below)
+    }
+    if (lane == 0) bl = FO::one_mont();
+    const T g = wave_pow_scan<FO>(b64, lane);  // base^(64 (lane+1))
+    for (uint32_t q = 1; q < nq; ++q) {
+      T gq;
+#pragma unroll
+      for (int w = 0; w < FO::NW; ++w) gq.w[w] = __shfl(g.w[w], (int)(q - 1), 64);
+      const uint32_t i = 64 * q + lane;
+      if (i < n && lane != 0) tab[i] = FO::mul(gq, bl);
+      if (i < n && lane == 0) tab[i] = gq;
+    }
+  }
+}
+
+// Block-wide modular sums of three values per thread (wave shuffles, then across waves in LDS).
+template <class FO>
+DEVI void block_sum3(typename FO::T& a, typename FO::T& b, typename FO::T& c, typename FO::T* red,
+                     uint32_t tid, uint32_t nthr) {
+  using T = typename FO::T;
+  T v[3] = {a, b, c};
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      T o;
+#pragma unroll
+      for (int w = 0; w < FO::NW; ++w) o.w[w] = __shfl_xor(v[q].w[w], off, 64);
+      v[q] = FO::add(v[q], o);
+    }
+  }
+  const uint32_t wave = tid >> 6, nw = (nthr + 63) >> 6;
+  if ((tid & 63) == 0) {
+    red[3 * wave + 0] = v[0];
+    red[3 * wave + 1] = v[1];
+    red[3 * wave + 2] = v[2];
   }
   __syncthreads();
-  for (uint32_t s = 2; s < n; s <<= 1) {
-    const typename FO::T h = tab[s >> 1];
-    const typename FO::T bs = FO::mul(h, h);  // base^s
-    for (uint32_t i = tid; i < s && i + s < n; i += nthr) tab[i + s] = FO::mul(tab[i], bs);
-    __syncthreads();
+  T r0 = red[0], r1 = red[1], r2 = red[2];
+  for (uint32_t w = 1; w < nw; ++w) {
+    r0 = FO::add(r0, red[3 * w + 0]);
+    r1 = FO::add(r1, red[3 * w + 1]);
+    r2 = FO::add(r2, red[3 * w + 2]);
   }
+  __syncthreads();
+  a = r0;
+  b = r1;
+  c = r2;
 }
 
 struct FlpDims {
@@ -412,7 +480,8 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
   T* PA = RP + dims.rp_len;
   T* PB = PA + H * c;
   T* RED = PB + H * c;
-  uint32_t* flag = reinterpret_cast<uint32_t*>(RED + nthr);
+  T* PW = RED + nthr;  // 128-entry scratch for the power tables
+  uint32_t* flag = reinterpret_cast<uint32_t*>(PW + 128);
   if (tid == 0) *flag = 0u;
 
   const uint8_t* xr = meas.at(r);
@@ -420,20 +489,25 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
   const uint32_t arity = cfg.arity;
   const uint32_t gp_len = cfg.gp_len;
 
-  // ---- powers of t (Montgomery): TP[i] = t^i, i < 2m ----
+  // ---- power tables (Montgomery), one wave each, concurrently:  TP[i] = t^i (i < 2m);
+  //      RP[i] = r^i (i <= c, or <= calls for Sum);  MM[k] = (r^c)^(k-1) (k = 1..calls) ----
   const T tm = FO::to_mont(FO::load(tq.at(r)));
-  pow_table<FO>(TP, tm, 2 * m, tid, nthr);
-  // ---- r powers ----
   T rm = FO::one_mont();
   if (cfg.jr_len > 0) rm = FO::to_mont(FO::load(jr.at(r)));
-  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
-    // RP[i] = r^i (i <= c);  MM[k] = (r^c)^(k-1) (k = 1..calls), multiplied by L_k below
-    pow_table<FO>(RP, rm, c + 1, tid, nthr);
-    const T rc = RP[c];
-    pow_table<FO>(MM + 1, rc, cfg.calls, tid, nthr);
-  } else if (cfg.kind == KIND_SUM) {
-    pow_table<FO>(RP, rm, cfg.calls + 1, tid, nthr);  // RP[k] = r^k
+  {
+    const uint32_t wave = tid >> 6, lane = tid & 63, nw = nthr >> 6;
+    const bool psum = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM);
+    if (wave == 0) wave_pow_table<FO>(TP, tm, 2 * m, lane);
+    if (wave == (nw > 1 ? 1u : 0u)) {
+      if (psum) wave_pow_table<FO>(RP, rm, c + 1, lane);
+      else if (cfg.kind == KIND_SUM) wave_pow_table<FO>(RP, rm, cfg.calls + 1, lane);
+    }
+    if (psum && wave == (nw > 2 ? 2u : 0u)) {
+      const T rc = mont_pow<FO>(rm, c);  // r^c (each lane, in parallel)
+      wave_pow_table<FO>(MM + 1, rc, cfg.calls, lane);
+    }
   }
+  __syncthreads();
   // ---- NTT inputs: NA <- t^(m-1-i) (bit-reversed), NB <- folded gadget poly (bit-reversed) ----
   bool bad = false;
   for (uint32_t i = tid; i < m; i += nthr) {
@@ -476,9 +550,7 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
     else gsum = FO::add(gsum, NB[k]);
     lsum = FO::add(lsum, LM[k]);
   }
-  pt = block_sum<FO>(pt, RED, tid, nthr);
-  gsum = block_sum<FO>(gsum, RED, tid, nthr);
-  lsum = block_sum<FO>(lsum, RED, tid, nthr);
+  block_sum3<FO>(pt, gsum, lsum, RED, tid, nthr);
 
   // ---- main loop: wire accumulations over the measurement share ----
   T xsum = FO::zero();  // Histogram sum check
