@@ -66,7 +66,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sumvec", choices=list(CONFIGS))
     ap.add_argument("--reports", type=int, default=0, help="reports per GPU per step (B)")
-    ap.add_argument("--unique", type=int, default=0, help="distinct synthetic reports per rank")
+    ap.add_argument("--unique", type=int, default=0, help="CPU-baseline sample size (reports)")
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -93,13 +93,10 @@ def main():
     from oracle.ref import Prio3Ref
 
     kind, bits, length, chunk, label = CONFIGS[args.config]
-    defaults = {"sumvec": (262144, 8192), "sum": (1 << 20, 16384), "histogram": (1 << 20, 16384),
+    defaults = {"sumvec": (262144, 4096), "sum": (1 << 20, 16384), "histogram": (1 << 20, 16384),
                 "count": (1 << 22, 65536)}
     B = args.reports or defaults[args.config][0]
     U = args.unique or defaults[args.config][1]
-    U = min(U, B)
-    if B % U:
-        B = (B // U) * U
     cfg_id = f"bench-{args.config}".encode()
     import hashlib
     vk = hashlib.shake_128(b"verify-key" + cfg_id).digest(16)
@@ -107,21 +104,33 @@ def main():
     vdaf = Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=local_rank)
     s = vdaf.sizes
 
-    # ---- synthetic inputs: U distinct reports per rank (C restatement client), tiled to B ------
+    # ---- synthetic inputs: B distinct reports per rank (SURVEY §8(d) recipe).  The recipe's
+    # nonces / client randomness / measurements come from the C restatement (multithreaded); the
+    # shares are made by the GPU client (prio3gpu_shard: Client::shard + FLP prove).  A sample is
+    # checked against the C restatement's own shard before anything is timed.
     ref = Prio3Ref(kind, vk, bits, length, chunk)
     t0 = time.time()
-    gen = ref.gen(cfg_id, rank * U, U, threads=args.gen_threads)
+    syn = ref.synth(cfg_id, rank * B, B, threads=args.gen_threads)
+    d_nonces = torch.from_numpy(syn["nonces"]).to(dev)
+    d_meas = torch.from_numpy(syn["meas"].view(np.int64)).to(dev)
+    d_rand = torch.from_numpy(syn["rand"]).to(dev)
+    d_pub = torch.empty((B, s.public_share), dtype=torch.uint8, device=dev) if s.public_share \
+        else None
+    d_lin = torch.empty((B, s.leader_input_share), dtype=torch.uint8, device=dev)
+    d_hin = torch.empty((B, s.helper_input_share), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    hs0 = vdaf.new_state(1, B)
+    vdaf.shard(hs0, d_nonces, d_meas, d_rand, out=(d_pub, d_lin, d_hin))
+    hs0.close()
+    del d_rand
     gen_s = time.time() - t0
-    tiles = B // U
-
-    def to_dev(a):
-        t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        return t.repeat(tiles, *([1] * (t.dim() - 1))).contiguous() if tiles > 1 else t
-
-    d_nonces = to_dev(gen["nonces"])
-    d_pub = to_dev(gen["public"]) if s.public_share else None
-    d_lin = to_dev(gen["leader_in"])
-    d_hin = to_dev(gen["helper_in"])
+    U = min(U, B)  # CPU-baseline sample size
+    chk = ref.gen(cfg_id, rank * B, min(U, 64), threads=args.gen_threads)
+    k = chk["nonces"].shape[0]
+    assert np.array_equal(d_lin[:k].cpu().numpy(), chk["leader_in"]), "GPU shard != C shard"
+    assert np.array_equal(d_hin[:k].cpu().numpy(), chk["helper_in"]), "GPU shard != C shard"
+    if s.public_share:
+        assert np.array_equal(d_pub[:k].cpu().numpy(), chk["public"]), "GPU shard != C shard"
     d_lprep = torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
     d_msgs = torch.empty((B, max(1, s.prep_msg)), dtype=torch.uint8, device=dev)
     d_lst = torch.zeros(B, dtype=torch.uint8, device=dev)
@@ -191,13 +200,13 @@ def main():
     ha, hc = hagg.read(0)
     exp_count = total_steps * B * world
     assert lc == exp_count and hc == exp_count, (lc, hc, exp_count)
-    meas = gen["meas"]
+    meas = syn["meas"]
     if kind == 2:
-        plain = [int(x) * tiles * total_steps for x in meas.sum(axis=0)]
+        plain = [int(x) * total_steps for x in meas.sum(axis=0, dtype=np.uint64)]
     elif kind == 3:
-        plain = [int((meas[:, 0] == i).sum()) * tiles * total_steps for i in range(length)]
+        plain = [int((meas[:, 0] == i).sum()) * total_steps for i in range(length)]
     else:
-        plain = int(meas[:, 0].sum()) * tiles * total_steps
+        plain = int(meas[:, 0].sum()) * total_steps
     if dist is not None:  # every rank holds the merged totals: compare with all ranks' plaintext
         allp = [None] * world
         dist.all_gather_object(allp, plain)
@@ -248,25 +257,32 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        cn = d_nonces[:U].cpu().numpy()
+        cp = d_pub[:U].cpu().numpy() if d_pub is not None else np.zeros((U, 0), np.uint8)
+        cl = d_lin[:U].cpu().numpy()
+        ch = d_hin[:U].cpu().numpy()
         done, t0 = 0, time.perf_counter()
         while True:
-            res = ref.prepare_batch(gen["nonces"], gen["public"], gen["leader_in"],
-                                    gen["helper_in"], threads=nthr, outputs=False)
+            res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=False)
             assert res["count"] == U
             done += U
             if time.perf_counter() - t0 >= args.cpu_seconds:
                 break
         cpu_s = time.perf_counter() - t0
-        # cross-check the CPU restatement's aggregate with the GPU's (GPU = tiles*steps copies)
-        p = vdaf.modulus
-        mult = tiles * total_steps
-        gl = [(x * mult) % p for x in vdaf.decode_field_vec(res["agg_l"].tobytes())]
-        assert gl == vdaf.decode_field_vec(la), "GPU leader aggregate != CPU restatement"
+        # the CPU restatement's aggregate over the sample == plaintext sum of the sample
+        sm = syn["meas"][:U]
+        if kind == 2:
+            sp = [int(x) for x in sm.sum(axis=0, dtype=np.uint64)]
+        elif kind == 3:
+            sp = [int((sm[:, 0] == i).sum()) for i in range(length)]
+        else:
+            sp = int(sm[:, 0].sum())
+        assert vdaf.unshard([res["agg_l"].tobytes(), res["agg_h"].tobytes()]) == sp
         cpu = {"value": round(done / cpu_s, 2), "unit": "reports/s", "cores": nthr,
                "kind": "port",
-               "sample": f"{done} reports ({U} distinct, repeated) leader+helper prepare+aggregate, "
-                         f"{nthr} threads, {cpu_s:.1f} s; C restatement of prio 0.15.1 "
-                         f"(reference not buildable)"}
+               "sample": f"{done} report preparations ({U} distinct reports, repeated) leader+helper "
+                         f"prepare+aggregate, {nthr} threads, {cpu_s:.1f} s; C restatement of "
+                         f"prio 0.15.1 (reference not buildable)"}
 
     out = {
         "metric": METRIC if args.config == "sumvec" else f"reports/sec prepared+aggregated, {label}",
@@ -280,8 +296,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u128 (Field128 mod p)" if s.field_size == 16 else "u64 (Field64 mod p)",
-        "data": f"synthetic: {U} distinct reports/rank (SURVEY §8(d) recipe) tiled x{tiles}, "
-                f"resident in HBM",
+        "data": f"synthetic: {B} distinct reports/GPU (SURVEY §8(d) recipe; shares made by the GPU "
+                f"client shard), resident in HBM",
         "config": {"workload": label, "reports_per_gpu_per_step": B,
                    "parallelism": f"report-sharded x{world}, RCCL all-gather merge"},
         "roofline": roof,

@@ -153,6 +153,19 @@ int prio3gpu_helper_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const 
                          const uint8_t* leader_prep_shares, const uint32_t* batch_slots,
                          uint8_t* out_prep_msgs, uint8_t* status, prio3gpu_agg* agg);
 
+/* Client::shard for n reports (prio 0.15.1 shard_with_random; SURVEY §8(f) #1: batched client
+ * shard + FLP prove, used to generate inputs at scale).
+ *   measurements  n x (SUMVEC ? length : 1) u64 (Count 0/1, Sum value, SumVec entries, Histogram
+ *                 bucket index)
+ *   rand          n x prio3gpu_random_size() bytes, prio order:
+ *                 k_meas, k_proof, [blind_helper, blind_leader], k_prove
+ *   outputs       public shares, leader input shares, helper input shares (DAP encodings)
+ * `st` must be a helper (agg_id 1) state of sufficient capacity; it is used as scratch. */
+int prio3gpu_random_size(const prio3gpu_ctx* ctx);
+int prio3gpu_shard(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const uint8_t* nonces,
+                   const uint64_t* measurements, const uint8_t* rand, uint8_t* out_public,
+                   uint8_t* out_leader, uint8_t* out_helper);
+
 /* Multi-GPU merge of per-GPU partial aggregates (one process per GPU).  RCCL all-gather of the
  * raw field-element bytes over xGMI, then a mod-p add kernel (RCCL sum is neither modular nor
  * 128-bit).  Counts are summed with an RCCL uint64 all-reduce.

@@ -64,6 +64,8 @@ def _declare(lib):
         "prio3gpu_prepare_shares_to_prepare_message": (c.c_int, [P, c.c_size_t, u8p, u8p, u8p, u8p]),
         "prio3gpu_prepare_next": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, P, P]),
         "prio3gpu_helper_init": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, u8p, P, u8p, u8p, P]),
+        "prio3gpu_random_size": (c.c_int, [P]),
+        "prio3gpu_shard": (c.c_int, [P, P, c.c_size_t, u8p, P, u8p, u8p, u8p, u8p]),
         "prio3gpu_comm_unique_id": (c.c_int, [u8p]),
         "prio3gpu_comm_init": (c.c_int, [u8p, c.c_int, c.c_int, c.c_int, c.POINTER(P)]),
         "prio3gpu_comm_destroy": (c.c_int, [P]),
@@ -90,7 +92,7 @@ EXPORTED = [
     "prio3gpu_agg_create", "prio3gpu_agg_destroy", "prio3gpu_agg_reset", "prio3gpu_agg_read",
     "prio3gpu_agg_merge_bytes", "prio3gpu_prepare_init",
     "prio3gpu_prepare_shares_to_prepare_message", "prio3gpu_prepare_next", "prio3gpu_helper_init",
-    "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
+    "prio3gpu_random_size", "prio3gpu_shard", "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
     "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
     "prio3gpu_prof_kernel_name", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
     "prio3gpu_last_error",

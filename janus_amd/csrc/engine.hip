@@ -127,11 +127,11 @@ struct DevBuf {
 
 enum KernelId {
   KID_QUERY = 0, KID_EXPAND, KID_JR, KID_FLP, KID_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_MERGE,
-  KID_OUT, KID_MERGE, KID_COUNT
+  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_jr", "k_flp_query", "k_decide", "k_prepare_next",
-    "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge"};
+    "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge", "k_shard_*", "k_flp_prove"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -162,7 +162,7 @@ struct prio3gpu_ctx {
   uint8_t vk[16];
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf twiddles;
+  DevBuf twiddles, twiddles2;
   // generic staging (inputs given as host pointers) and scratch
   DevBuf io[6];
   DevBuf perm, chunks, partials, pcounts;
@@ -325,6 +325,21 @@ int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_
   CHK(c->twiddles.ensure(tw.size()));
   HIPCHK(hipMemcpy(c->twiddles.p, tw.data(), tw.size(), hipMemcpyHostToDevice));
   g.twiddles = c->twiddles.u8();
+  // prover table: w^k (k < 2m, w = primitive 2m-th root), 1/m, 1/(2m); Montgomery
+  {
+    const uint32_t m2 = 2 * g.m;
+    const u128 w = powmod(7, (p - 1) / m2, p);
+    std::vector<uint8_t> t2((size_t)(m2 + 2) * es);
+    u128 x = 1;
+    for (uint32_t k = 0; k < m2 + 2; ++k) {
+      u128 v = k < m2 ? x : (k == m2 ? p - (p - 1) / g.m : p - (p - 1) / m2);
+      u128 mv = mulmod(v, R, p);
+      for (uint32_t b = 0; b < es; ++b) t2[(size_t)k * es + b] = (uint8_t)(mv >> (8 * b));
+      x = mulmod(x, w, p);
+    }
+    CHK(c->twiddles2.ensure(t2.size()));
+    HIPCHK(hipMemcpy(c->twiddles2.p, t2.data(), t2.size(), hipMemcpyHostToDevice));
+  }
   return 0;
 }
 
@@ -609,6 +624,7 @@ int prio3gpu_ctx_destroy(prio3gpu_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->twiddles.release();
+  c->twiddles2.release();
   for (auto& b : c->io) b.release();
   c->perm.release();
   c->chunks.release();
@@ -933,6 +949,128 @@ int prio3gpu_helper_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const ui
   CHK(copy_out(c, out_prep_msgs, d_msg, n * g.prep_msg_len));
   CHK(copy_out(c, status, d_status, n));
   HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_random_size(const prio3gpu_ctx* c) {
+  if (!c) return PRIO3GPU_E_ARG;
+  return 16 * (3 + (c->cfg.jr_len ? 2 : 0));
+}
+
+}  // extern "C"
+
+namespace {
+template <class FO>
+int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
+                 const uint64_t* d_meas, uint32_t mw, const uint8_t* d_rand, uint8_t* d_pub,
+                 uint8_t* d_leader, uint8_t* d_helper) {
+  const Cfg& g = c->cfg;
+  const uint32_t N = (uint32_t)n, es = g.es;
+  const size_t rs = (size_t)prio3gpu_random_size(c);
+  // scratch: helper meas/proof (state), proof + prove rand + jr (state buffers reused)
+  CHK(st->prep.ensure(n * (size_t)g.proof_len * es));       // full proof
+  CHK(st->jr.ensure(n * (size_t)std::max<uint32_t>(g.prove_rand_len, 1) * es + n * 32));
+  uint8_t* d_proof = st->prep.u8();
+  uint8_t* d_prand = st->jr.u8();
+  uint8_t* d_jr = d_prand + n * (size_t)std::max<uint32_t>(g.prove_rand_len, 1) * es;
+  Rows helper{d_helper, g.helper_share_len}, leader{d_leader, g.leader_share_len};
+  {
+    PROF(KID_SHARD);
+    hipLaunchKernelGGL(k_shard_seeds, grid1(n, 256), dim3(256), 0, c->stream, g, N,
+                       CRows{d_rand, rs}, helper, leader);
+  }
+  Rows hm{st->meas.u8(), (size_t)g.meas_len * es}, hp{st->proof.u8(), (size_t)g.proof_len * es};
+  {
+    PROF(KID_EXPAND);
+    hipLaunchKernelGGL(k_expand<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, 1u,
+                       CRows{d_helper, g.helper_share_len}, hm, hp, (const uint8_t*)nullptr);
+  }
+  {
+    PROF(KID_SHARD);
+    hipLaunchKernelGGL(k_shard_meas<FO>, dim3((g.meas_len + 255) / 256, N), dim3(256), 0,
+                       c->stream, g, N, d_meas, mw, CRows{hm.base, hm.stride}, leader);
+    hipLaunchKernelGGL(k_shard_jr<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N,
+                       CRows{d_nonces, 16}, CRows{d_rand, rs}, CRows{hm.base, hm.stride},
+                       CRows{d_leader, g.leader_share_len}, Rows{d_pub, g.public_share_len},
+                       Rows{d_jr, 32}, Rows{d_prand, (size_t)std::max<uint32_t>(g.prove_rand_len, 1) * es});
+  }
+  {
+    PROF(KID_PROVE);
+    const uint32_t cc = (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM) ? g.chunk : 1u;
+    const size_t lds = sizeof(typename FO::T) * (8 * (size_t)g.m + cc + 1 + g.calls + 1) + 16;
+    if (lds > 160 * 1024) {
+      set_err("prove LDS requirement %zu too large", lds);
+      return PRIO3GPU_E_ARG;
+    }
+    hipLaunchKernelGGL(k_flp_prove<FO>, dim3(N), dim3(256), lds, c->stream, g, N,
+                       c->twiddles2.u8(), d_meas, mw,
+                       CRows{d_prand, (size_t)std::max<uint32_t>(g.prove_rand_len, 1) * es},
+                       CRows{d_jr, 32}, Rows{d_proof, (size_t)g.proof_len * es});
+  }
+  {
+    PROF(KID_SHARD);
+    hipLaunchKernelGGL(k_shard_proof<FO>, dim3((g.proof_len + 255) / 256, N), dim3(256), 0,
+                       c->stream, g, N, CRows{d_proof, (size_t)g.proof_len * es},
+                       CRows{hp.base, hp.stride}, leader);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int prio3gpu_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* nonces,
+                   const uint64_t* measurements, const uint8_t* rand, uint8_t* out_public,
+                   uint8_t* out_leader, uint8_t* out_helper) {
+  CHK(check_state(c, st, n));
+  if (st->agg_id != 1) {
+    set_err("shard needs a helper-shaped (agg_id 1) state for scratch");
+    return PRIO3GPU_E_ARG;
+  }
+  if (n == 0) return 0;
+  if (!nonces || !measurements || !rand || !out_leader || !out_helper ||
+      (c->cfg.jr_len && !out_public)) {
+    set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const Cfg& g = c->cfg;
+  const uint32_t mw = g.kind == KIND_SUMVEC ? g.length : 1u;
+  const size_t rs = (size_t)prio3gpu_random_size(c);
+  const uint8_t *d_nonces, *d_meas, *d_rand;
+  CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));
+  CHK(stage_in(c, st->pub, measurements, n * (size_t)mw * 8, &d_meas));
+  CHK(stage_in(c, st->input, rand, n * rs, &d_rand));
+  // outputs: device pointers written in place, host pointers staged
+  uint8_t* d_out[3];
+  void* host_out[3] = {out_public, out_leader, out_helper};
+  const size_t out_len[3] = {n * g.public_share_len, n * (size_t)g.leader_share_len,
+                             n * (size_t)g.helper_share_len};
+  for (int i = 0; i < 3; ++i) {
+    if (!host_out[i] || out_len[i] == 0) {
+      d_out[i] = nullptr;
+      continue;
+    }
+    if (is_device_ptr(host_out[i])) {
+      d_out[i] = static_cast<uint8_t*>(host_out[i]);
+    } else {
+      CHK(c->io[i].ensure(out_len[i]));
+      d_out[i] = c->io[i].u8();
+    }
+  }
+  int rc;
+  if (is_f64(c))
+    rc = launch_shard<Field64Ops>(c, st, n, d_nonces, reinterpret_cast<const uint64_t*>(d_meas),
+                                  mw, d_rand, d_out[0], d_out[1], d_out[2]);
+  else
+    rc = launch_shard<Field128Ops>(c, st, n, d_nonces, reinterpret_cast<const uint64_t*>(d_meas),
+                                   mw, d_rand, d_out[0], d_out[1], d_out[2]);
+  if (rc) return rc;
+  for (int i = 0; i < 3; ++i)
+    if (d_out[i] && d_out[i] != host_out[i]) CHK(copy_out(c, host_out[i], d_out[i], out_len[i]));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  st->n = 0;  // scratch was used for sharding, not a prepared batch
   return 0;
 }
 

@@ -871,3 +871,250 @@ __global__ void __launch_bounds__(256) k_merge(uint8_t* dst, const uint8_t* src,
 }
 
 }  // namespace p3g
+
+namespace p3g {
+
+// =================================================================================================
+// Client: batched Prio3 shard + FLP prove (prio 0.15.1 Prio3::shard_with_random,
+// flp.rs Type::prove).  Used to generate inputs at scale; the aggregator path does not depend on it.
+// =================================================================================================
+
+// Encoded measurement element i (0/1 for every type here) from the raw measurement row
+// (SumVec: `length` u64 entries, others: one u64).  prio Type::encode_measurement.
+DEVI uint32_t enc_meas_bit(const Cfg& cfg, const uint64_t* m, uint32_t i) {
+  switch (cfg.kind) {
+    case KIND_COUNT: return (uint32_t)(m[0] & 1u);
+    case KIND_SUM: return (uint32_t)((m[0] >> i) & 1u);
+    case KIND_SUMVEC: return (uint32_t)((m[i / cfg.bits] >> (i % cfg.bits)) & 1u);
+    default: return m[0] == i ? 1u : 0u;  // Histogram one-hot
+  }
+}
+
+// Radix-2 DIT NTT of size n over up to two LDS arrays (inputs bit-reversed), twiddles
+// omega_N^(k*stride) from a table of N-th roots (Montgomery).  All threads call.
+template <class FO>
+DEVI void ntt_lds(typename FO::T* A, typename FO::T* B, uint32_t n, uint32_t logn,
+                  const uint8_t* tw, uint32_t stride, uint32_t tid, uint32_t nthr) {
+  const uint32_t na = B ? 2u : 1u;
+  for (uint32_t st = 1; st <= logn; ++st) {
+    const uint32_t half = 1u << (st - 1);
+    for (uint32_t q = tid; q < na * (n >> 1); q += nthr) {
+      typename FO::T* a = q < (n >> 1) ? A : B;
+      const uint32_t bq = q & ((n >> 1) - 1u);
+      const uint32_t grp = bq >> (st - 1), k = bq & (half - 1u);
+      const uint32_t i = grp * 2u * half + k, j = i + half;
+      const typename FO::T w = FO::load(tw + (size_t)((k << (logn - st)) * stride) * FO::ES);
+      const typename FO::T u = a[i];
+      const typename FO::T v = FO::mul(w, a[j]);
+      a[i] = FO::add(u, v);
+      a[j] = FO::sub(u, v);
+    }
+    __syncthreads();
+  }
+}
+
+// FLP prove, one block per report.  Everything in Montgomery form until the final conversion.
+// Wire polys interpolate f_{w,k} (k = 0: prove rand seed; 1..calls: recorded gadget inputs with
+// num_shares = 1; zero above).  The gadget poly G(f_0..f_{arity-1}) has degree 2(m-1): its values
+// at the 2m-th roots are, at even points, G of the recorded values and, at odd points w*alpha^k,
+// G of the wire polys' values there (iNTT -> twist by w^d / m -> NTT).  Interpolating those 2m
+// values gives the 2m-1 proof coefficients.
+// tw2 = [w^0 .. w^(2m-1), 1/m, 1/(2m)] (w = primitive 2m-th root), Montgomery.
+// LDS: FA[m] FB[m] GA[m] GB[m] PE[m] PO[m] G[2m] RP[c+1] RR[calls+1]
+template <class FO>
+__global__ void __launch_bounds__(256) k_flp_prove(Cfg cfg, uint32_t n, const uint8_t* tw2,
+                                                   const uint64_t* meas, uint32_t meas_words,
+                                                   CRows prove_rand, CRows jr, Rows proof_out) {
+  using T = typename FO::T;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t r = blockIdx.x;
+  if (r >= n) return;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  const uint32_t m = cfg.m, logm = cfg.logm, calls = cfg.calls;
+  const uint32_t c = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) ? cfg.chunk : 1u;
+  T* FA = reinterpret_cast<T*>(smem);
+  T* FB = FA + m;
+  T* GA = FB + m;
+  T* GB = GA + m;
+  T* PE = GB + m;
+  T* PO = PE + m;
+  T* G = PO + m;
+  T* RP = G + 2 * m;
+  T* RR = RP + (c + 1);
+  const uint64_t* mrow = meas + (size_t)r * meas_words;
+  const uint8_t* pr = prove_rand.at(r);
+  const T one = FO::one_mont();
+  const T inv_m = FO::load(tw2 + (size_t)(2 * m) * FO::ES);
+  const T inv_2m = FO::load(tw2 + (size_t)(2 * m + 1) * FO::ES);
+  const bool psum = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM);
+  // r powers for the a-wires (ParallelSum types): RP[i] = r^i (i <= c), RR[q] = (r^c)^q
+  {
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    T rm = one;
+    if (psum) rm = FO::to_mont(FO::load(jr.at(r)));
+    if (psum && wave == 0) wave_pow_table<FO>(RP, rm, c + 1, lane);
+    if (psum && wave == (nthr > 64 ? 1u : 0u)) {
+      const T rc = mont_pow<FO>(rm, c);
+      wave_pow_table<FO>(RR, rc, calls, lane);
+    }
+  }
+  for (uint32_t k = tid; k < m; k += nthr) {
+    PE[k] = FO::zero();
+    PO[k] = FO::zero();
+  }
+  __syncthreads();
+  const uint32_t npairs = psum ? c : 1u;  // Sum: one wire; Count: one (x, x) pair
+  for (uint32_t j = 0; j < npairs; ++j) {
+    // wire values at alpha^k, written bit-reversed for the interpolating NTT
+    for (uint32_t k = tid; k < m; k += nthr) {
+      T a = FO::zero(), b = FO::zero();
+      if (k == 0) {
+        if (cfg.kind == KIND_SUM) {
+          a = FO::to_mont(FO::load(pr));
+        } else {
+          a = FO::to_mont(FO::load(pr + (size_t)(2 * j) * FO::ES));
+          b = FO::to_mont(FO::load(pr + (size_t)(2 * j + 1) * FO::ES));
+        }
+      } else if (k <= calls) {
+        if (psum) {
+          const uint32_t idx = (k - 1) * c + j;
+          if (idx < cfg.meas_len) {
+            const uint32_t x = enc_meas_bit(cfg, mrow, idx);
+            a = x ? FO::mul(RP[j + 1], RR[k - 1]) : FO::zero();  // r^(idx+1) x
+            b = x ? FO::zero() : FO::neg(one);                  // x - 1
+          } else {
+            b = FO::neg(one);  // padding (0, -1/num_shares), num_shares = 1
+          }
+        } else if (cfg.kind == KIND_SUM) {
+          a = enc_meas_bit(cfg, mrow, k - 1) ? one : FO::zero();
+        } else {  // Count: Mul(x, x)
+          a = enc_meas_bit(cfg, mrow, 0) ? one : FO::zero();
+          b = a;
+        }
+      }
+      // even gadget values
+      if (cfg.kind == KIND_SUM) PE[k] = FO::add(PE[k], FO::sub(FO::mul(a, a), a));
+      else PE[k] = FO::add(PE[k], FO::mul(a, b));
+      const uint32_t br = bitrev(k, logm);
+      FA[br] = a;
+      FB[br] = b;
+    }
+    __syncthreads();
+    ntt_lds<FO>(FA, cfg.kind == KIND_SUM ? nullptr : FB, m, logm, tw2, 2, tid, nthr);
+    // coefficients c_d = X[(m-d) mod m] / m ; twist by w^d ; bit-reverse for the next NTT
+    for (uint32_t d = tid; d < m; d += nthr) {
+      const uint32_t src = (m - d) & (m - 1);
+      const T s = FO::mul(FO::load(tw2 + (size_t)d * FO::ES), inv_m);
+      const uint32_t br = bitrev(d, logm);
+      GA[br] = FO::mul(FA[src], s);
+      if (cfg.kind != KIND_SUM) GB[br] = FO::mul(FB[src], s);
+    }
+    __syncthreads();
+    ntt_lds<FO>(GA, cfg.kind == KIND_SUM ? nullptr : GB, m, logm, tw2, 2, tid, nthr);
+    for (uint32_t k = tid; k < m; k += nthr) {
+      const T a = GA[k];
+      if (cfg.kind == KIND_SUM) PO[k] = FO::add(PO[k], FO::sub(FO::mul(a, a), a));
+      else PO[k] = FO::add(PO[k], FO::mul(a, GB[k]));
+    }
+    __syncthreads();
+  }
+  // interpolate the gadget poly from its 2m values: G[2k] = PE[k], G[2k+1] = PO[k]
+  const uint32_t logm2 = logm + 1, m2 = 2 * m;
+  for (uint32_t i = tid; i < m2; i += nthr) G[bitrev(i, logm2)] = (i & 1) ? PO[i >> 1] : PE[i >> 1];
+  __syncthreads();
+  ntt_lds<FO>(G, nullptr, m2, logm2, tw2, 1, tid, nthr);
+  uint8_t* out = proof_out.at(r);
+  const uint32_t arity = cfg.arity;
+  for (uint32_t d = tid; d < cfg.gp_len; d += nthr) {
+    const T v = FO::mul(G[(m2 - d) & (m2 - 1)], inv_2m);
+    FO::store(out + (size_t)(arity + d) * FO::ES, FO::from_mont(v));
+  }
+  for (uint32_t w = tid; w < arity; w += nthr)
+    FO::store(out + (size_t)w * FO::ES, FO::load(pr + (size_t)w * FO::ES));
+}
+
+// Shard helpers (lane per report).  rand row = [k_meas, k_proof, (blind_h, blind_l,) k_prove].
+// helper share = [k_meas, k_proof, (blind_h)], leader share tail = blind_l.
+__global__ void __launch_bounds__(256) k_shard_seeds(Cfg cfg, uint32_t n, CRows rand,
+                                                     Rows helper, Rows leader) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint8_t* rd = rand.at(r);
+  uint8_t* h = helper.at(r);
+  for (int i = 0; i < 4; ++i) st64(h + 8 * i, ld64(rd + 8 * i));
+  if (cfg.jr_len) {
+    st64(h + 32, ld64(rd + 32));
+    st64(h + 40, ld64(rd + 40));
+    uint8_t* l = leader.at(r) + (size_t)(cfg.meas_len + cfg.proof_len) * cfg.es;
+    st64(l, ld64(rd + 48));
+    st64(l + 8, ld64(rd + 56));
+  }
+}
+
+// leader meas share = encode(measurement) - helper meas share   (elementwise; thread per element)
+template <class FO>
+__global__ void __launch_bounds__(256) k_shard_meas(Cfg cfg, uint32_t n, const uint64_t* meas,
+                                                    uint32_t meas_words, CRows helper_meas,
+                                                    Rows leader) {
+  const uint32_t r = blockIdx.y;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n || i >= cfg.meas_len) return;
+  const uint32_t x = enc_meas_bit(cfg, meas + (size_t)r * meas_words, i);
+  const typename FO::T h = FO::load(helper_meas.at(r) + (size_t)i * FO::ES);
+  FO::store(leader.at(r) + (size_t)i * FO::ES, FO::sub(FO::from_u32(x), h));
+}
+
+// Both joint-rand parts, the public share, the joint-rand seed and the joint randomness; then the
+// prove randomness XOF(k_prove, dst4, "").  Lane per report.
+template <class FO>
+__global__ void __launch_bounds__(256) k_shard_jr(Cfg cfg, uint32_t n, CRows nonces, CRows rand,
+                                                  CRows helper_meas, CRows leader, Rows pub,
+                                                  Rows jr_out, Rows prove_rand_out) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint8_t* nz = nonces.at(r);
+  const uint8_t* rd = rand.at(r);
+  const uint32_t kp = cfg.jr_len ? 64u : 32u;  // offset of k_prove in the rand row
+  if (cfg.jr_len) {
+    uint64_t hlo, hhi, llo, lhi;
+    jr_part(cfg.algo_id, 1, ld64(rd + 32), ld64(rd + 40), ld64(nz), ld64(nz + 8),
+            helper_meas.at(r), cfg.meas_len * cfg.es, hlo, hhi);
+    jr_part(cfg.algo_id, 0, ld64(rd + 48), ld64(rd + 56), ld64(nz), ld64(nz + 8), leader.at(r),
+            cfg.meas_len * cfg.es, llo, lhi);
+    uint8_t* p = pub.at(r);
+    st64(p, llo);
+    st64(p + 8, lhi);
+    st64(p + 16, hlo);
+    st64(p + 24, hhi);
+    uint64_t slo, shi;
+    derive_jr_seed(cfg.algo_id, llo, lhi, hlo, hhi, slo, shi);
+    MsgBlock mb;
+    mb.clear();
+    mb.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
+    mb.pad(25);
+    uint64_t s[25];
+    sponge_one_block<24>(s, mb);
+    squeeze_vec<FO, 24>(s, cfg.jr_len, jr_out.at(r));
+  }
+  MsgBlock mb;
+  mb.clear();
+  mb.header(cfg.algo_id, DST_PROVE_RANDOMNESS, ld64(rd + kp), ld64(rd + kp + 8));
+  mb.pad(25);
+  uint64_t s[25];
+  sponge_one_block<24>(s, mb);
+  squeeze_vec<FO, 24>(s, cfg.prove_rand_len, prove_rand_out.at(r));
+}
+
+// leader proof share = proof - helper proof share   (thread per element)
+template <class FO>
+__global__ void __launch_bounds__(256) k_shard_proof(Cfg cfg, uint32_t n, CRows proof,
+                                                     CRows helper_proof, Rows leader) {
+  const uint32_t r = blockIdx.y;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n || i >= cfg.proof_len) return;
+  const typename FO::T a = FO::load(proof.at(r) + (size_t)i * FO::ES);
+  const typename FO::T h = FO::load(helper_proof.at(r) + (size_t)i * FO::ES);
+  FO::store(leader.at(r) + (size_t)(cfg.meas_len + i) * FO::ES, FO::sub(a, h));
+}
+
+}  // namespace p3g

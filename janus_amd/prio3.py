@@ -274,6 +274,28 @@ class Prio3Gpu:
                                          agg._h if agg else None), "helper_init")
         return msgs, st
 
+    # -- Client ------------------------------------------------------------------------------------
+    def random_size(self) -> int:
+        return lib().prio3gpu_random_size(self._ctx)
+
+    def shard(self, state: PrepareState, nonces, measurements, rand, out=None):
+        """Batched `Client::shard` (prio shard_with_random) on the GPU -> (public shares, leader
+        input shares, helper input shares).  `measurements`: (n,) or (n, length) uint64."""
+        s = self.sizes
+        n = _nbytes(nonces) // 16
+        nonces = _as_u8(nonces, n, 16, "nonces")
+        rand = _as_u8(rand, n, self.random_size(), "rand")
+        if isinstance(measurements, np.ndarray):
+            measurements = np.ascontiguousarray(measurements, dtype=np.uint64)
+        if out is None:
+            out = (np.zeros((n, s.public_share), np.uint8) if s.public_share else None,
+                   np.zeros((n, s.leader_input_share), np.uint8),
+                   np.zeros((n, s.helper_input_share), np.uint8))
+        pub, lead, helper = out
+        check(lib().prio3gpu_shard(self._ctx, state._h, n, _ptr(nonces), _ptr(measurements),
+                                   _ptr(rand), _ptr(pub), _ptr(lead), _ptr(helper)), "shard")
+        return pub, lead, helper
+
     # -- Collector ---------------------------------------------------------------------------------
     def decode_field_vec(self, b: bytes):
         es = self.sizes.field_size

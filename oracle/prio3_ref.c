@@ -887,3 +887,46 @@ void p3ref_shake128(const u8* msg, size_t len, u8* out, size_t outlen) {
   shake_finish(&h);
   shake_squeeze(&h, out, outlen);
 }
+
+/* Synthetic report inputs only (nonce, client randomness, measurement) per the SURVEY §8(d)
+ * recipe, for n reports from index `start`; the shares are then produced by prio3gpu_shard. */
+typedef struct {
+  const p3ref* r;
+  const u8* cfg_id;
+  size_t cfg_len;
+  u64 start;
+  size_t lo, hi;
+  u8 *nonces, *rand;
+  u64* meas;
+} synth_job;
+
+static void* synth_worker(void* arg) {
+  synth_job* j = (synth_job*)arg;
+  const cfgt* c = &j->r->c;
+  const unsigned rs = p3ref_random_size(c);
+  const unsigned mw = c->kind == K_SUMVEC ? c->length : 1;
+  u128* enc = (u128*)malloc(sizeof(u128) * c->meas_len);
+  for (size_t k = j->lo; k < j->hi; ++k)
+    synth(c, j->cfg_id, j->cfg_len, j->start + k, j->nonces + 16 * k, j->rand + (size_t)rs * k, enc,
+          j->meas + (size_t)mw * k);
+  free(enc);
+  return NULL;
+}
+
+int p3ref_synth(const p3ref* r, const u8* cfg_id, size_t cfg_len, u64 start, size_t n, int threads,
+                u8* nonces, u8* rand, u64* meas) {
+  if (threads < 1) threads = 1;
+  synth_job* jobs = (synth_job*)calloc(threads, sizeof(synth_job));
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  for (int t = 0; t < threads; ++t) {
+    synth_job* j = &jobs[t];
+    j->r = r; j->cfg_id = cfg_id; j->cfg_len = cfg_len; j->start = start;
+    j->lo = n * t / threads; j->hi = n * (t + 1) / threads;
+    j->nonces = nonces; j->rand = rand; j->meas = meas;
+    pthread_create(&th[t], NULL, synth_worker, j);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+  return 0;
+}

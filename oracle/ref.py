@@ -32,6 +32,9 @@ def lib():
         l.p3ref_gen.restype = ctypes.c_int
         l.p3ref_gen.argtypes = [P, P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_size_t,
                                 ctypes.c_int, P, P, P, P, P]
+        l.p3ref_synth.restype = ctypes.c_int
+        l.p3ref_synth.argtypes = [P, P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_size_t,
+                                  ctypes.c_int, P, P, P]
         l.p3ref_prepare_batch.restype = ctypes.c_longlong
         l.p3ref_prepare_batch.argtypes = [P, ctypes.c_size_t, ctypes.c_int] + [P] * 10
         _lib = l
@@ -73,6 +76,17 @@ class Prio3Ref:
         lib().p3ref_gen(self._h, _p(cid), len(cfg_id), start, n, threads, _p(out["nonces"]),
                         _p(out["public"]) if self.public_len else None, _p(out["leader_in"]),
                         _p(out["helper_in"]), _p(out["meas"]))
+        return out
+
+    def synth(self, cfg_id: bytes, start: int, n: int, threads: int = 0):
+        """Inputs only (nonces, client randomness, measurements) for n synthetic reports."""
+        threads = threads or (os.cpu_count() or 1)
+        cid = np.frombuffer(cfg_id, dtype=np.uint8).copy()
+        out = dict(nonces=np.zeros((n, 16), np.uint8),
+                   rand=np.zeros((n, self.random_size), np.uint8),
+                   meas=np.zeros((n, self.length if self.kind == 2 else 1), np.uint64))
+        lib().p3ref_synth(self._h, _p(cid), len(cfg_id), start, n, threads, _p(out["nonces"]),
+                          _p(out["rand"]), _p(out["meas"]))
         return out
 
     def prepare_batch(self, nonces, public, leader_in, helper_in, threads=1, outputs=True):

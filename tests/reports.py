@@ -46,6 +46,7 @@ class Batch:
     prep_msg: np.ndarray
     leader_out: np.ndarray
     helper_out: np.ndarray
+    rand: np.ndarray = None
 
 
 def _pack(rows: List[bytes], width: int) -> np.ndarray:
@@ -62,12 +63,13 @@ def make_batch(name: str, n: int, cfg_id: bytes = None, start: int = 0) -> Batch
     keys = ["public_share", "leader_input_share", "helper_input_share", "leader_prep_share",
             "helper_prep_share", "prep_msg", "leader_out_share", "helper_out_share"]
     cols = {k: [] for k in keys}
-    nonces, meas = [], []
+    nonces, meas, rands = [], [], []
     for i in range(start, start + n):
         nonce, m, rand = O.synth_report(v, cfg_id, i)
         t = O.run_vdaf(v, vk, nonce, m, rand)
         nonces.append(nonce)
         meas.append(m)
+        rands.append(rand)
         for k in keys:
             cols[k].append(t[k])
     es = v.fld.ENCODED_SIZE
@@ -82,7 +84,15 @@ def make_batch(name: str, n: int, cfg_id: bytes = None, start: int = 0) -> Batch
         prep_msg=_pack(cols["prep_msg"], v.prep_msg_len()),
         leader_out=_pack(cols["leader_out_share"], v.typ.OUTPUT_LEN * es),
         helper_out=_pack(cols["helper_out_share"], v.typ.OUTPUT_LEN * es),
+        rand=_pack(rands, v.random_size()),
     )
+
+
+def meas_array(b: Batch) -> np.ndarray:
+    """Measurements as the (n, words) uint64 array prio3gpu_shard takes."""
+    if isinstance(b.measurements[0], list):
+        return np.array(b.measurements, dtype=np.uint64)
+    return np.array(b.measurements, dtype=np.uint64).reshape(-1, 1)
 
 
 def expected_aggregate(b: Batch, which: str, mask=None, slots=None, slot=0) -> bytes:

@@ -223,3 +223,18 @@ def test_rccl_merge_single_rank():
     assert got == expected_aggregate(b, "leader")[0] and cnt == b.n
     assert local.read(0)[1] == 0
     comm.close()
+
+
+@pytest.mark.parametrize("name", list(SIZES))
+def test_gpu_shard_matches_oracle(name):
+    """Client::shard + FLP prove on the GPU reproduce the oracle's public/leader/helper shares."""
+    from tests.reports import meas_array
+    b = batch(name)
+    v = gpu_vdaf(b)
+    assert v.random_size() == b.rand.shape[1]
+    st = v.new_state(1, b.n)
+    pub, lead, helper = v.shard(st, b.nonces, meas_array(b), b.rand)
+    np.testing.assert_array_equal(helper, b.helper_in)
+    if v.sizes.public_share:
+        np.testing.assert_array_equal(pub, b.public)
+    np.testing.assert_array_equal(lead, b.leader_in)
