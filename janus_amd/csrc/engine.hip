@@ -127,11 +127,12 @@ struct DevBuf {
 
 enum KernelId {
   KID_QUERY = 0, KID_EXPAND, KID_JR, KID_FLP, KID_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_MERGE,
-  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_COUNT
+  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_FLP_WIRES, KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_jr", "k_flp_query", "k_decide", "k_prepare_next",
-    "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge", "k_shard_*", "k_flp_prove"};
+    "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge", "k_shard_*", "k_flp_prove",
+    "k_flp_wires"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -197,7 +198,7 @@ struct prio3gpu_state {
   int agg_id = 0;
   size_t cap = 0;
   size_t n = 0;
-  DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input;
+  DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input, w;
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
 };
 
@@ -405,16 +406,19 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   if (g.jr_len > 0) {
     {
       PROF(KID_JR);
-      hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
+      hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), (TPB / 64) * kJrWaveLds, c->stream, g, N,
                          (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
                          Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status);
     }
   }
-  // FLP query: block per report
+  // FLP query: block per report.  ParallelSum types (SumVec, Histogram) split it in two: the
+  // weights (power tables, NTTs, gadget outputs; latency-bound, 2 waves) and the wire pass over
+  // the measurement share (HBM streaming, many blocks in flight).
   FlpDims dims;
   uint32_t nthr;
   dims.rp_len = std::max(g.chunk, g.calls) + 1;
-  if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM) {
+  const bool psum = (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM);
+  if (psum) {
     dims.cols = g.chunk;
     if (g.chunk <= 256) {
       dims.H = 256 / g.chunk;
@@ -427,20 +431,43 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   } else {
     dims.cols = 1;
     dims.H = 1;
-    nthr = (g.kind == KIND_SUM) ? 64 : 64;
+    nthr = 64;
   }
   const size_t esz = sizeof(typename FO::T);
-  size_t lds = esz * (6 * (size_t)g.m + dims.rp_len + 2 * (size_t)dims.H * dims.cols + nthr + 128) + 16;
+  FlpDims d1 = dims;
+  uint32_t nthr1 = nthr;
+  if (psum) {
+    d1.H = 0;
+    nthr1 = 128;
+  }
+  size_t lds = esz * (6 * (size_t)g.m + d1.rp_len + 2 * (size_t)d1.H * d1.cols + nthr1 + 128) + 16;
   lds = (lds + 15) & ~(size_t)15;
   if (lds > 160 * 1024) {
     set_err("FLP LDS requirement %zu too large", lds);
     return PRIO3GPU_E_ARG;
   }
-  {
+  Rows wrows{nullptr, 0};
+  if (psum) wrows = Rows{st->w.u8(), (size_t)flp_w_len(g) * es};
+  if (psum && g.m <= 128 && g.chunk <= 128) {
     PROF(KID_FLP);
-    hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr), lds, c->stream, g, N, dims, meas, proof,
+    hipLaunchKernelGGL(k_flp_weights<FO>, grid1(n, 4), dim3(256), 0, c->stream, g, N, proof,
                        CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status);
+                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
+                       wrows);
+  } else {
+    PROF(KID_FLP);
+    hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr1), lds, c->stream, g, N, d1, meas, proof,
+                       CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
+                       wrows);
+  }
+  if (psum) {
+    size_t lds2 = esz * (2 * (size_t)g.calls + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
+    lds2 = (lds2 + 15) & ~(size_t)15;
+    PROF(KID_FLP_WIRES);
+    hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
+                       CRows{wrows.base, wrows.stride}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                       Rows{st->prep.u8(), g.prep_share_len}, d_status);
   }
   HIPCHK(hipGetLastError());
   st->meas_rows = meas;
@@ -676,6 +703,8 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   rc |= st->prep.ensure(N * g.prep_share_len);
   rc |= st->msg.ensure(N * 16);
   rc |= st->status.ensure(N);
+  if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM)
+    rc |= st->w.ensure(N * (size_t)flp_w_len(g) * g.es);
   if (agg_id == 1) {
     rc |= st->meas.ensure(N * (size_t)g.meas_len * g.es);
     rc |= st->proof.ensure(N * (size_t)g.proof_len * g.es);
@@ -692,7 +721,7 @@ int prio3gpu_state_destroy(prio3gpu_state* st) {
   if (!st) return 0;
   if (st->ctx) (void)hipStreamSynchronize(st->ctx->stream);
   for (DevBuf* b : {&st->t, &st->jr, &st->part, &st->seed, &st->meas, &st->proof, &st->prep,
-                    &st->msg, &st->status, &st->nonces, &st->pub, &st->input})
+                    &st->msg, &st->status, &st->nonces, &st->pub, &st->input, &st->w})
     b->release();
   delete st;
   return 0;

@@ -272,19 +272,106 @@ __global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t ag
 
 // Joint randomness (prio prepare_init): own part over the encoded meas share, corrected seed
 // (public-share parts with this aggregator's part replaced), joint_rand = XOF(seed, dst3, "").
+//
+// The meas share is streamed through LDS: each wave owns a 64 x 176-byte window (one 168-byte
+// rate block of every lane's report plus the preceding word), filled for block b+1 by 11 LDS-DMA
+// instructions (global_load_lds_dwordx4, 16 B/lane, ~6 rows per instruction instead of 64) while
+// block b is permuted.  All lanes of a wave take part in the fill, so lanes past n or with a
+// failed status still run the loop (on a clamped row) and just do not store.
+constexpr uint32_t kJrWin = 176;  // bytes per report in the LDS window (22 words)
+constexpr uint32_t kJrWaveLds = 64 * kJrWin;
+
 template <class FO>
 __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id, CRows nonces,
                                             CRows public_shares, CRows blinds, CRows meas,
                                             Rows out_part, Rows out_seed, Rows out_jr,
                                             const uint8_t* status) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  if (status && status[r] != ST_OK) return;
-  const uint8_t* nz = nonces.at(r);
-  const uint8_t* bl = blinds.at(r);
-  uint64_t plo, phi;
-  jr_part(cfg.algo_id, agg_id, ld64(bl), ld64(bl + 8), ld64(nz), ld64(nz + 8), meas.at(r),
-          cfg.meas_len * cfg.es, plo, phi);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t r0w = blockIdx.x * blockDim.x + (tid & ~63u);  // first report of this wave
+  if (r0w >= n) return;                                          // wave-uniform
+  const uint32_t r = r0w + lane;
+  const bool live = r < n && (!status || status[r] == ST_OK);
+  const uint32_t rr = r < n ? r : n - 1u;
+  uint8_t* win = smem + (tid >> 6) * kJrWaveLds;
+
+  const uint8_t* nz = nonces.at(rr);
+  const uint8_t* bl = blinds.at(rr);
+  const uint64_t nonce_lo = ld64(nz), nonce_hi = ld64(nz + 8);
+  const uint8_t* data = meas.at(rr);
+  const uint32_t nbytes = cfg.meas_len * cfg.es;
+  MsgBlock pre;
+  pre.clear();
+  pre.header(cfg.algo_id, DST_JOINT_RAND_PART, ld64(bl), ld64(bl + 8));
+  pre.put8(25, agg_id);
+  pre.put64(26, nonce_lo);
+  pre.put64(34, nonce_hi);
+  const int64_t nd = nbytes / 8;
+  const int64_t total = 42 + (int64_t)nbytes;
+  const int64_t nblocks = total / 168 + 1;
+  const int64_t padw = total >> 3;
+  const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
+
+  // LDS-DMA piece q of this lane: flat piece P = 64q + lane = (row, k) with 11 pieces per row
+  uint32_t voff[11];
+#pragma unroll
+  for (int q = 0; q < 11; ++q) {
+    const uint32_t P = 64u * q + lane;
+    const uint32_t row = P / 11u, k = P - row * 11u;
+    const uint32_t rowc = (r0w + row < n ? r0w + row : n - 1u) - r0w;
+    voff[q] = rowc * (uint32_t)meas.stride + 16u * k;
+  }
+  const uint8_t* wbase = meas.base + (size_t)r0w * meas.stride;
+  auto is_fast = [&](int64_t b) { return (b >= 1) && (21 * b + 15 < nd) && (21 * b + 20 < padw); };
+  auto stage = [&](int64_t b) {  // window <- words [21b-6, 21b+16) of every row of the wave
+    const uint8_t* src = wbase + 8 * (21 * b - 6);
+#pragma unroll
+    for (int q = 0; q < 11; ++q)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + voff[q]),
+          (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, 0, 0);
+  };
+
+  uint64_t s[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) s[i] = 0ull;
+  for (int64_t b = 0; b < nblocks; ++b) {
+    if (is_fast(b)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t* L = reinterpret_cast<const uint64_t*>(win + lane * kJrWin);
+      uint64_t prev = L[0];
+#pragma unroll
+      for (int w = 0; w < 21; ++w) {
+        const uint64_t cur = L[w + 1];
+        s[w] ^= (prev >> 48) | (cur << 16);
+        prev = cur;
+      }
+    } else if (b == 0) {
+#pragma unroll
+      for (int w = 0; w < 21; ++w) {
+        uint64_t v = (w < 5) ? pre.w[w] : jr_data_word(w, data, nd, nonce_hi);
+        if (padw == w) v ^= padv;
+        if (nblocks == 1 && w == 20) v ^= 0x8000000000000000ull;
+        s[w] ^= v;
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 21; ++w) {
+        const int64_t g = 21 * b + w;
+        uint64_t v = jr_data_word(g, data, nd, nonce_hi);
+        if (padw == g) v ^= padv;
+        if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
+        s[w] ^= v;
+      }
+    }
+    if (is_fast(b + 1)) {  // refill the window (its reads above have completed) under the permutation
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stage(b + 1);
+    }
+    keccak_p<24>(s);
+  }
+  if (!live) return;
+  const uint64_t plo = s[0], phi = s[1];
   st64(out_part.at(r), plo);
   st64(out_part.at(r) + 8, phi);
   const uint8_t* ps = public_shares.at(r);
@@ -304,9 +391,9 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
   m.clear();
   m.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
   m.pad(25);
-  uint64_t s[25];
-  sponge_one_block<24>(s, m);
-  squeeze_vec<FO, 24>(s, cfg.jr_len, out_jr.at(r));
+  uint64_t s2[25];
+  sponge_one_block<24>(s2, m);
+  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -460,10 +547,14 @@ struct FlpDims {
   uint32_t rp_len;  // entries of the r-power table RP
 };
 
+// W row written by k_flp_query in split mode (ParallelSum types) and read by k_flp_wires:
+//   MM[1..calls] | LM[1..calls] | RP[1..c] | B0[c] = L0 s_2j | B1[c] = L0 s_2j+1 - (1/2) sum L_k | gsum
+__host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + 3 * cfg.chunk + 1; }
+
 template <class FO>
 __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
                                                    CRows proof, CRows tq, CRows jr, CRows part,
-                                                   Rows out_prep, uint8_t* status) {
+                                                   Rows out_prep, uint8_t* status, Rows wrows) {
   using T = typename FO::T;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t r = blockIdx.x;
@@ -556,6 +647,40 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
   T xsum = FO::zero();  // Histogram sum check
   uint8_t* outp = out_prep.at(r);
   const size_t ES = FO::ES;
+  if ((cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) && wrows.base != nullptr) {
+    // split mode: hand the weights to k_flp_wires (which streams the measurement share)
+    uint8_t* wr = wrows.at(r);
+    const uint32_t C = cfg.calls;
+    for (uint32_t k = tid; k < C; k += nthr) {
+      FO::store(wr + (size_t)k * ES, MM[k + 1]);
+      FO::store(wr + (size_t)(C + k) * ES, LM[k + 1]);
+    }
+    const T l0 = LM[0];
+    const T half_l = FO::mul(lsum, FO::half());
+    for (uint32_t j = tid; j < c; j += nthr) {
+      const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
+      const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
+      bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
+      FO::store(wr + (size_t)(2 * C + j) * ES, RP[j + 1]);  // Montgomery
+      FO::store(wr + (size_t)(2 * C + c + j) * ES, FO::mul(l0, s0));
+      FO::store(wr + (size_t)(2 * C + 2 * c + j) * ES, FO::sub(FO::mul(l0, s1), half_l));
+    }
+    if (bad) atomicOr(flag, 1u);
+    __syncthreads();
+    if (tid == 0) {
+      FO::store(wr + (size_t)(2 * C + 3 * c) * ES, gsum);
+      if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
+      FO::store(outp + (size_t)(1 + arity) * ES, pt);
+      const uint8_t* pp = part.at(r);
+      uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
+      st64(dst, ld64(pp));
+      st64(dst + 8, ld64(pp + 8));
+      const uint32_t f = *flag;
+      if (f & 1u) status[r] = ST_INVALID_MESSAGE;
+      else if (f & 2u) status[r] = ST_VDAF_PREP_ERROR;
+    }
+    return;
+  }
   if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
     for (uint32_t slot = tid; slot < H * c; slot += nthr) {
       const uint32_t j = slot % c, h = slot / c;
@@ -663,6 +788,316 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
     const uint32_t f = *flag;
     if (f & 1u) status[r] = ST_INVALID_MESSAGE;
     else if (f & 2u) status[r] = ST_VDAF_PREP_ERROR;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// FLP query, ParallelSum types, first half, one WAVE per report (m <= 128, chunk <= 128): the same
+// weights as k_flp_query's split mode, computed in registers with cross-lane shuffles instead of
+// LDS tables and block barriers (no LDS at all, so occupancy is set by VGPRs alone):
+//   * powers of t, r and r^c by wave product scans;
+//   * both size-m NTTs (t^(m-1-i) and the folded gadget poly) as register DIF transforms:
+//     position p = 64e + lane, stage distance h = 64 in-lane, h < 64 via shfl_xor; the result at
+//     position p is X[bitrev(p)], which is the k the lane stores under;
+//   * p(t) with lane l summing coefficients d = l + 64q.
+// ------------------------------------------------------------------------------------------------
+template <class FO>
+DEVI typename FO::T shfl_T(const typename FO::T& v, int src) {
+  typename FO::T o;
+#pragma unroll
+  for (int w = 0; w < FO::NW; ++w) o.w[w] = __shfl(v.w[w], src, 64);
+  return o;
+}
+template <class FO>
+DEVI typename FO::T shfl_xor_T(const typename FO::T& v, int mask) {
+  typename FO::T o;
+#pragma unroll
+  for (int w = 0; w < FO::NW; ++w) o.w[w] = __shfl_xor(v.w[w], mask, 64);
+  return o;
+}
+template <class FO>
+DEVI typename FO::T wave_sum(typename FO::T v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = FO::add(v, shfl_xor_T<FO>(v, off));
+  return v;
+}
+template <class FO>
+DEVI typename FO::T sel(bool c, const typename FO::T& a, const typename FO::T& b) {
+  typename FO::T o;
+#pragma unroll
+  for (int w = 0; w < FO::NW; ++w) o.w[w] = c ? a.w[w] : b.w[w];
+  return o;
+}
+
+template <class FO>
+__global__ void __launch_bounds__(256) k_flp_weights(Cfg cfg, uint32_t n, CRows proof, CRows tq,
+                                                     CRows jr, CRows part, Rows out_prep,
+                                                     uint8_t* status, Rows wrows) {
+  using T = typename FO::T;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= n) return;              // wave-uniform
+  if (status[r] != ST_OK) return;  // wave-uniform
+  const uint32_t m = cfg.m, logm = cfg.logm, C = cfg.calls, c = cfg.chunk;
+  const uint32_t arity = cfg.arity, gp_len = cfg.gp_len;
+  const size_t ES = FO::ES;
+  const uint8_t* pr = proof.at(r);
+  const uint8_t* gp = pr + (size_t)arity * ES;
+  const T one = FO::one_mont();
+  bool bad = false;
+
+  // ---- powers of t:  tl = t^lane,  t64 = t^64 ----
+  const T tm = FO::to_mont(FO::load(tq.at(r)));
+  const T ta = wave_pow_scan<FO>(tm, lane);  // t^(lane+1)
+  T tl = shfl_T<FO>(ta, (int)((lane + 63u) & 63u));
+  tl = sel<FO>(lane == 0, one, tl);
+  const T t64 = shfl_T<FO>(ta, 63);
+  const T t128 = FO::mul(t64, t64);
+  const T tmm = shfl_T<FO>(tl, (int)(m & 63u));  // t^m for m < 64
+  const bool tbad = FO::eq(m == 128 ? t128 : (m == 64 ? t64 : tmm), one);
+
+  // ---- gadget poly coefficients d = lane + 64q (q < 4), p(t) partial sums ----
+  T cd[4];
+  T pt = FO::zero();
+  {
+    T tp = tl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t d = lane + 64u * q;
+      cd[q] = FO::zero();
+      if (d < gp_len) {
+        cd[q] = FO::load(gp + (size_t)d * ES);
+        bad |= !FO::is_canonical(cd[q]);
+        pt = FO::add(pt, FO::mul(tp, cd[q]));
+      }
+      if (q < 3) tp = FO::mul(tp, t64);
+    }
+  }
+  pt = wave_sum<FO>(pt);
+
+  // ---- NTT inputs (natural order), position p = 64e + lane ----
+  T A[2], B[2];
+  {
+    const T S = shfl_T<FO>(tl, (int)((m - 1u - lane) & 63u));  // t^((m-1-lane) mod 64)
+    if (m == 128) {
+      A[0] = FO::mul(S, t64);  // t^(127-lane)
+      A[1] = S;                // t^(63-lane)
+      B[0] = FO::add(cd[0], cd[2]);
+      B[1] = FO::add(cd[1], cd[3]);
+    } else if (m == 64) {
+      A[0] = S;
+      A[1] = FO::zero();
+      B[0] = FO::add(cd[0], cd[1]);
+      B[1] = FO::zero();
+    } else {  // m < 64: fold c_(l+m) from lane l+m
+      const T up = shfl_T<FO>(cd[0], (int)((lane + m) & 63u));
+      A[0] = lane < m ? S : FO::zero();
+      B[0] = lane < m ? (lane + m < gp_len ? FO::add(cd[0], up) : cd[0]) : FO::zero();
+      A[1] = FO::zero();
+      B[1] = FO::zero();
+    }
+  }
+  // ---- DIF NTTs: X[k] = sum_i x_i alpha_m^(ik), output at bitrev position ----
+  if (m == 128) {
+    const T w = ld_tw<FO>(cfg, lane);  // alpha_128^lane
+    T u = A[0], v = A[1];
+    A[0] = FO::add(u, v);
+    A[1] = FO::mul(FO::sub(u, v), w);
+    u = B[0];
+    v = B[1];
+    B[0] = FO::add(u, v);
+    B[1] = FO::mul(FO::sub(u, v), w);
+  }
+  const uint32_t E = m == 128 ? 2u : 1u;
+  for (uint32_t h = (m >= 64 ? 32u : m >> 1); h >= 1; h >>= 1) {
+    const T w = ld_tw<FO>(cfg, (lane & (h - 1u)) * (m / (2u * h)));
+    const bool hi = (lane & h) != 0;
+#pragma unroll
+    for (uint32_t e = 0; e < 2; ++e) {
+      if (e < E) {
+        const T oa = shfl_xor_T<FO>(A[e], (int)h), ob = shfl_xor_T<FO>(B[e], (int)h);
+        const T sa = hi ? FO::sub(oa, A[e]) : FO::add(A[e], oa);
+        const T sb = hi ? FO::sub(ob, B[e]) : FO::add(B[e], ob);
+        A[e] = hi ? FO::mul(sa, w) : sa;
+        B[e] = hi ? FO::mul(sb, w) : sb;
+      }
+    }
+  }
+  // ---- Lagrange weights LM[k] = Y_k alpha^k / m, gadget outputs G[k] = B ----
+  const T inv_m = ld_tw<FO>(cfg, m);
+  uint32_t K[2];
+  T LMv[2];
+  T lsum = FO::zero(), gsum = FO::zero();
+#pragma unroll
+  for (uint32_t e = 0; e < 2; ++e) {
+    const uint32_t p = 64u * e + lane;
+    K[e] = bitrev(p & (m - 1u), logm);
+    LMv[e] = FO::mul(FO::mul(A[e], ld_tw<FO>(cfg, K[e])), inv_m);
+    if (e < E && p < m && K[e] >= 1u && K[e] <= C) {
+      lsum = FO::add(lsum, LMv[e]);
+      gsum = FO::add(gsum, B[e]);
+    }
+  }
+  lsum = wave_sum<FO>(lsum);
+  gsum = wave_sum<FO>(gsum);
+  const T l0 = shfl_T<FO>(LMv[0], 0);  // position 0 holds k = 0 (lane 0, e = 0)
+
+  // ---- r powers: RP[j] = r^j,  rc = r^c,  MM[k] = LM[k] rc^(k-1) ----
+  const T rm = FO::to_mont(FO::load(jr.at(r)));
+  const T ra = wave_pow_scan<FO>(rm, lane);  // r^(lane+1)
+  const T r64 = shfl_T<FO>(ra, 63);
+  T rc = shfl_T<FO>(ra, (int)((c - 1u) & 63u));
+  if (c > 64) rc = FO::mul(rc, r64);
+  const T qa = wave_pow_scan<FO>(rc, lane);  // rc^(lane+1)
+  T ql = shfl_T<FO>(qa, (int)((lane + 63u) & 63u));
+  ql = sel<FO>(lane == 0, one, ql);  // rc^lane
+  const T q64 = shfl_T<FO>(qa, 63);
+  uint8_t* wr = wrows.at(r);
+#pragma unroll
+  for (uint32_t e = 0; e < 2; ++e) {
+    const uint32_t p = 64u * e + lane;
+    const uint32_t k = K[e];
+    const T qk = shfl_T<FO>(ql, (int)((k - 1u) & 63u));  // all lanes shuffle, then select
+    if (e < E && p < m && k >= 1u && k <= C) {
+      T mm = FO::mul(LMv[e], qk);
+      if (k - 1u >= 64u) mm = FO::mul(mm, q64);
+      FO::store(wr + (size_t)(k - 1u) * ES, mm);
+      FO::store(wr + (size_t)(C + k - 1u) * ES, LMv[e]);
+    }
+  }
+  const T half_l = FO::mul(lsum, FO::half());
+#pragma unroll
+  for (uint32_t q = 0; q < 2; ++q) {
+    const uint32_t j = lane + 64u * q;
+    if (j < c) {
+      FO::store(wr + (size_t)(2 * C + j) * ES, q ? FO::mul(ra, r64) : ra);  // r^(j+1), Montgomery
+      const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
+      const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
+      bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
+      FO::store(wr + (size_t)(2 * C + c + j) * ES, FO::mul(l0, s0));
+      FO::store(wr + (size_t)(2 * C + 2 * c + j) * ES, FO::sub(FO::mul(l0, s1), half_l));
+    }
+  }
+  const bool anybad = __any(bad);
+  if (lane == 0) {
+    FO::store(wr + (size_t)(2 * C + 3 * c) * ES, gsum);
+    uint8_t* outp = out_prep.at(r);
+    if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
+    FO::store(outp + (size_t)(1 + arity) * ES, pt);
+    const uint8_t* pp = part.at(r);
+    uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
+    st64(dst, ld64(pp));
+    st64(dst + 8, ld64(pp + 8));
+    if (anybad) status[r] = ST_INVALID_MESSAGE;
+    else if (tbad) status[r] = ST_VDAF_PREP_ERROR;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// FLP query, ParallelSum types, second half: stream the measurement share once and form the wires
+//   wire_2j   = B0[j] + r^(j+1) sum_k MM[k] x_(k-1)c+j      wire_2j+1 = B1[j] + sum_k LM[k] x_(k-1)c+j
+// (weights from k_flp_query's split mode).  Block per report, thread (h, j): column j, calls
+// k = 1+h, 1+h+H, ...; lazy-reduced 256-bit MACs, two measurement loads in flight per thread.
+// ------------------------------------------------------------------------------------------------
+template <class FO>
+__global__ void __launch_bounds__(256) k_flp_wires(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
+                                                   CRows wrows, CRows jr, Rows out_prep,
+                                                   uint8_t* status) {
+  using T = typename FO::T;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t r = blockIdx.x;
+  if (r >= n) return;
+  if (status[r] != ST_OK) return;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  const uint32_t C = cfg.calls, c = dims.cols, H = dims.H;
+  const size_t ES = FO::ES;
+  T* MM = reinterpret_cast<T*>(smem);
+  T* LM = MM + C;
+  T* PA = LM + C;
+  T* PB = PA + H * c;
+  T* RED = PB + H * c;
+  uint32_t* flag = reinterpret_cast<uint32_t*>(RED + nthr);
+  if (tid == 0) *flag = 0u;
+  const uint8_t* wr = wrows.at(r);
+  for (uint32_t k = tid; k < 2 * C; k += nthr) MM[k] = FO::load(wr + (size_t)k * ES);
+  __syncthreads();
+  const uint8_t* xr = meas.at(r);
+  bool bad = false;
+  T xsum = FO::zero();
+  for (uint32_t slot = tid; slot < H * c; slot += nthr) {
+    const uint32_t j = slot % c, h = slot / c;
+    T accA, accB;
+    if constexpr (FO::ES == 16) {
+      Wide wa, wb;
+      wide_zero(wa);
+      wide_zero(wb);
+      uint32_t k = h;
+      for (; k + H < C; k += 2 * H) {  // calls k and k+H; only the last call can be padded
+        const uint32_t i0 = k * c + j, i1 = (k + H) * c + j;
+        const T x0 = FO::load(xr + (size_t)i0 * ES);
+        const T x1 = i1 < cfg.meas_len ? FO::load(xr + (size_t)i1 * ES) : FO::zero();
+        bad |= !FO::is_canonical(x0) || !FO::is_canonical(x1);
+        wide_mac(wa, MM[k], x0);
+        wide_mac(wb, LM[k], x0);
+        wide_mac(wa, MM[k + H], x1);
+        wide_mac(wb, LM[k + H], x1);
+        if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(FO::add(xsum, x0), x1);
+      }
+      if (k < C) {
+        const uint32_t i0 = k * c + j;
+        if (i0 < cfg.meas_len) {
+          const T x0 = FO::load(xr + (size_t)i0 * ES);
+          bad |= !FO::is_canonical(x0);
+          wide_mac(wa, MM[k], x0);
+          wide_mac(wb, LM[k], x0);
+          if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x0);
+        }
+      }
+      accA = wide_reduce(wa);
+      accB = wide_reduce(wb);
+    } else {
+      accA = FO::zero();
+      accB = FO::zero();
+      for (uint32_t k = h; k < C; k += H) {
+        const uint32_t idx = k * c + j;
+        if (idx < cfg.meas_len) {
+          const T x = FO::load(xr + (size_t)idx * ES);
+          bad |= !FO::is_canonical(x);
+          accA = FO::add(accA, FO::mul(MM[k], x));
+          accB = FO::add(accB, FO::mul(LM[k], x));
+          if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x);
+        }
+      }
+    }
+    PA[h * c + j] = accA;
+    PB[h * c + j] = accB;
+  }
+  __syncthreads();
+  uint8_t* outp = out_prep.at(r);
+  for (uint32_t j = tid; j < c; j += nthr) {
+    T a = FO::zero(), b = FO::zero();
+    for (uint32_t h = 0; h < H; ++h) {
+      a = FO::add(a, PA[h * c + j]);
+      b = FO::add(b, PB[h * c + j]);
+    }
+    const T rp = FO::load(wr + (size_t)(2 * C + j) * ES);  // Montgomery
+    const T w0 = FO::add(FO::load(wr + (size_t)(2 * C + c + j) * ES), FO::mul(rp, a));
+    const T w1 = FO::add(FO::load(wr + (size_t)(2 * C + 2 * c + j) * ES), b);
+    FO::store(outp + (size_t)(1 + 2 * j) * ES, w0);
+    FO::store(outp + (size_t)(2 + 2 * j) * ES, w1);
+  }
+  if (bad) atomicOr(flag, 1u);
+  if (cfg.kind == KIND_HISTOGRAM) xsum = block_sum<FO>(xsum, RED, tid, nthr);
+  __syncthreads();
+  if (tid == 0) {
+    if (cfg.kind == KIND_HISTOGRAM) {
+      // v = jr[1] * range + jr[1]^2 * (sum x - 1/2)
+      const T gsum = FO::load(wr + (size_t)(2 * C + 3 * c) * ES);
+      const T r1m = FO::to_mont(FO::load(jr.at(r) + ES));
+      const T sc = FO::sub(xsum, FO::half());
+      FO::store(outp, FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc)));
+    }
+    if (*flag & 1u) status[r] = ST_INVALID_MESSAGE;
   }
 }
 
