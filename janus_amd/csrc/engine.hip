@@ -127,12 +127,12 @@ struct DevBuf {
 
 enum KernelId {
   KID_QUERY = 0, KID_EXPAND, KID_JR, KID_FLP, KID_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_MERGE,
-  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_FLP_WIRES, KID_COUNT
+  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_FLP_WIRES, KID_ACC_SPEC, KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_jr", "k_flp_query", "k_decide", "k_prepare_next",
     "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge", "k_shard_*", "k_flp_prove",
-    "k_flp_wires"};
+    "k_flp_wires", "k_accum_spec"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -166,8 +166,9 @@ struct prio3gpu_ctx {
   DevBuf twiddles, twiddles2;
   // generic staging (inputs given as host pointers) and scratch
   DevBuf io[6];
-  DevBuf perm, chunks, partials, pcounts;
+  DevBuf perm, chunks, partials, pcounts, spec_idx;
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
+  bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
   Prof prof;
 };
 
@@ -200,6 +201,11 @@ struct prio3gpu_state {
   size_t n = 0;
   DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input, w;
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
+  // speculative accumulation: per-wave column sums of meas-share words, written by k_jr
+  DevBuf spec_lo, spec_cy;
+  bool spec_ok = false;
+  size_t spec_n = 0;
+  uint32_t spec_nd = 0, spec_e0 = 0, spec_e1 = 0;
 };
 
 struct prio3gpu_agg {
@@ -368,6 +374,23 @@ int copy_out(prio3gpu_ctx* c, void* dst, const void* dev_src, size_t bytes) {
 
 dim3 grid1(size_t n, uint32_t tpb) { return dim3((unsigned)((n + tpb - 1) / tpb)); }
 
+// Measurement-share words that k_jr absorbs through its LDS window ("fast" blocks 1..lf cover
+// words [16, 21 (lf+1) - 5)); elements [e0, e1) lie entirely inside.  Field128 types with JR only.
+bool spec_range(const Cfg& g, uint32_t& nd, uint32_t& e0, uint32_t& e1) {
+  if (g.es != 16 || g.jr_len == 0) return false;
+  const int64_t nbytes = (int64_t)g.meas_len * 16;
+  const int64_t ndw = nbytes / 8, padw = (42 + nbytes) >> 3;
+  auto is_fast = [&](int64_t b) { return b >= 1 && 21 * b + 15 < ndw && 21 * b + 20 < padw; };
+  int64_t lf = 0;
+  while (is_fast(lf + 1)) ++lf;
+  if (lf < 1) return false;
+  const int64_t f1 = (21 * (lf + 1) - 5) & ~(int64_t)1;
+  nd = (uint32_t)ndw;
+  e0 = 8;
+  e1 = (uint32_t)(f1 / 2);
+  return e1 > e0;
+}
+
 template <class FO>
 int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
                         const uint8_t* d_pub, const uint8_t* d_in, uint8_t* d_status) {
@@ -403,12 +426,29 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
     proof = CRows{po.base, po.stride};
     blinds = CRows{d_in + 32, g.helper_share_len};
   }
+  st->spec_ok = false;
+  uint64_t* spec_lo = nullptr;
+  uint8_t* spec_cy = nullptr;
+  uint32_t snd = 0, se0 = 0, se1 = 0;
+  if (g.jr_len > 0 && c->speculate && spec_range(g, snd, se0, se1)) {
+    const size_t nw = (n + 63) / 64;
+    CHK(st->spec_lo.ensure(nw * snd * 8));
+    CHK(st->spec_cy.ensure(nw * snd));
+    spec_lo = reinterpret_cast<uint64_t*>(st->spec_lo.p);
+    spec_cy = st->spec_cy.u8();
+    st->spec_ok = true;
+    st->spec_n = n;
+    st->spec_nd = snd;
+    st->spec_e0 = se0;
+    st->spec_e1 = se1;
+  }
   if (g.jr_len > 0) {
     {
       PROF(KID_JR);
       hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), (TPB / 64) * kJrWaveLds, c->stream, g, N,
                          (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
-                         Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status);
+                         Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status,
+                         spec_lo, spec_cy);
     }
   }
   // FLP query: block per report.  ParallelSum types (SumVec, Histogram) split it in two: the
@@ -494,7 +534,6 @@ template <class FO>
 int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint32_t* slots,
                       const uint8_t* d_status, prio3gpu_agg* agg) {
   const Cfg& g = c->cfg;
-  // host-side grouping by slot (stable counting sort)
   std::vector<uint32_t> hslots;
   const uint32_t* sl = slots;
   if (slots && is_device_ptr(slots)) {
@@ -504,56 +543,123 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
     sl = hslots.data();
   }
   const uint32_t S = agg->slots;
-  std::vector<uint32_t> cnt(S + 1, 0);
   for (size_t r = 0; r < n; ++r) {
-    uint32_t s = sl ? sl[r] : 0;
+    const uint32_t s = sl ? sl[r] : 0;
     if (s >= S) {
       set_err("batch slot %u out of range (%u slots)", s, S);
       return PRIO3GPU_E_ARG;
     }
-    cnt[s + 1]++;
   }
-  for (uint32_t s = 0; s < S; ++s) cnt[s + 1] += cnt[s];
-  auto& perm = c->h_perm;
-  perm.assign(n, 0);
-  {
-    std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
-    for (size_t r = 0; r < n; ++r) perm[pos[sl ? sl[r] : 0]++] = (uint32_t)r;
+  auto slot_of = [&](size_t r) -> uint32_t { return sl ? sl[r] : 0u; };
+  // Chunks (runs of reports of one slot, contiguous per slot in chunk order) of two kinds:
+  //  * direct: k_accum_partial sums every measurement element of the chunk's reports;
+  //  * speculative (whole waves of 64 reports whose slots agree, when k_jr left column sums):
+  //    k_accum_spec folds the per-wave sums of elements [e0, e1) and corrects the rejected rows,
+  //    k_accum_partial adds the few edge elements outside that range.
+  const bool spec = st->spec_ok && st->spec_n == n && FO::ES == 16;
+  const size_t nw = (n + 63) / 64;
+  std::vector<std::vector<uint32_t>> spec_w(S), direct_r(S);
+  if (spec) {
+    for (size_t w = 0; w < nw; ++w) {
+      const size_t r0 = 64 * w, r1 = std::min(n, r0 + 64);
+      const uint32_t s = slot_of(r0);
+      bool uni = true;
+      for (size_t r = r0 + 1; r < r1 && uni; ++r) uni = slot_of(r) == s;
+      if (uni) {
+        spec_w[s].push_back((uint32_t)w);
+      } else {
+        for (size_t r = r0; r < r1; ++r) direct_r[slot_of(r)].push_back((uint32_t)r);
+      }
+    }
+  } else {
+    for (size_t r = 0; r < n; ++r) direct_r[slot_of(r)].push_back((uint32_t)r);
   }
   const uint32_t epb = std::min<uint32_t>(256, std::max<uint32_t>(1, g.meas_len));
   const uint32_t G = 256 / epb;
   const uint32_t tiles = (g.meas_len + epb - 1) / epb;
   const size_t target_chunks = std::max<size_t>(1, 2048 / tiles);
-  size_t CH = std::max<size_t>((size_t)G * 4, (n + target_chunks - 1) / target_chunks);
+  const size_t CH = std::max<size_t>((size_t)G * 4, (n + target_chunks - 1) / target_chunks);
+  const size_t WCH = 32;  // waves per speculative chunk
+  auto& perm = c->h_perm;
   auto& cb = c->h_chunk_begin;
   auto& cs = c->h_chunk_slot;
+  perm.clear();
   cb.clear();
   cs.clear();
+  std::vector<uint32_t> dir_ids, spec_ids, swb, wl;
   for (uint32_t s = 0; s < S; ++s) {
-    for (size_t b = cnt[s]; b < cnt[s + 1]; b += CH) {
-      cb.push_back((uint32_t)b);
+    const auto& sw = spec_w[s];
+    for (size_t i = 0; i < sw.size(); i += WCH) {
+      spec_ids.push_back((uint32_t)cs.size());
+      cb.push_back((uint32_t)perm.size());
       cs.push_back(s);
+      swb.push_back((uint32_t)wl.size());
+      for (size_t q = i; q < std::min(sw.size(), i + WCH); ++q) {
+        wl.push_back(sw[q]);
+        for (size_t r = 64 * (size_t)sw[q]; r < std::min(n, 64 * (size_t)sw[q] + 64); ++r)
+          perm.push_back((uint32_t)r);
+      }
+    }
+    const auto& dr = direct_r[s];
+    for (size_t i = 0; i < dr.size(); i += CH) {
+      dir_ids.push_back((uint32_t)cs.size());
+      cb.push_back((uint32_t)perm.size());
+      cs.push_back(s);
+      perm.insert(perm.end(), dr.begin() + i, dr.begin() + std::min(dr.size(), i + CH));
     }
   }
   const uint32_t nch = (uint32_t)cs.size();
   if (nch == 0) return 0;
-  cb.push_back((uint32_t)n);
-  CHK(c->perm.ensure(n * 4));
+  cb.push_back((uint32_t)perm.size());
+  swb.push_back((uint32_t)wl.size());
+  const uint32_t ndir = (uint32_t)dir_ids.size(), nspec = (uint32_t)spec_ids.size();
+  CHK(c->perm.ensure(std::max<size_t>(1, perm.size()) * 4));
   CHK(c->chunks.ensure((size_t)(2 * nch + 1) * 4));
   CHK(c->partials.ensure((size_t)nch * g.meas_len * g.es));
   CHK(c->pcounts.ensure((size_t)nch * 4));
-  HIPCHK(hipMemcpyAsync(c->perm.p, perm.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  CHK(c->spec_idx.ensure((size_t)(ndir + 2 * nspec + 1 + wl.size() + 1) * 4));
+  HIPCHK(hipMemcpyAsync(c->perm.p, perm.data(), perm.size() * 4, hipMemcpyHostToDevice, c->stream));
   uint32_t* d_cb = reinterpret_cast<uint32_t*>(c->chunks.p);
   uint32_t* d_cs = d_cb + nch + 1;
   HIPCHK(hipMemcpyAsync(d_cb, cb.data(), (nch + 1) * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d_cs, cs.data(), nch * 4, hipMemcpyHostToDevice, c->stream));
-  // The host vectors must outlive the async copies: synchronise before they can be reused.
-  {
+  uint32_t* d_dir = reinterpret_cast<uint32_t*>(c->spec_idx.p);
+  uint32_t* d_sid = d_dir + ndir;
+  uint32_t* d_swb = d_sid + nspec;
+  uint32_t* d_wl = d_swb + nspec + 1;
+  if (ndir) HIPCHK(hipMemcpyAsync(d_dir, dir_ids.data(), ndir * 4, hipMemcpyHostToDevice, c->stream));
+  if (nspec) {
+    HIPCHK(hipMemcpyAsync(d_sid, spec_ids.data(), nspec * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_swb, swb.data(), (nspec + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_wl, wl.data(), wl.size() * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  const uint32_t* d_perm = reinterpret_cast<const uint32_t*>(c->perm.p);
+  uint32_t* d_pc = reinterpret_cast<uint32_t*>(c->pcounts.p);
+  const size_t red_lds = 256 * sizeof(typename FO::T) + 16;
+  if (ndir) {
     PROF(KID_ACC_PART);
-    hipLaunchKernelGGL(k_accum_partial<FO>, dim3(nch, tiles), dim3(256),
-                       256 * sizeof(typename FO::T) + 16, c->stream, g, st->meas_rows,
-                       reinterpret_cast<const uint32_t*>(c->perm.p), d_cb, d_status, epb,
-                       c->partials.u8(), reinterpret_cast<uint32_t*>(c->pcounts.p));
+    hipLaunchKernelGGL(k_accum_partial<FO>, dim3(ndir, tiles), dim3(256), red_lds, c->stream, g,
+                       st->meas_rows, d_perm, d_cb, d_status, epb, c->partials.u8(), d_pc, d_dir,
+                       g.meas_len, g.meas_len);
+  }
+  if (nspec) {
+    const uint32_t e0 = st->spec_e0, e1 = st->spec_e1;
+    const uint32_t nedge = e0 + (g.meas_len - e1);
+    const uint32_t epb_e = std::min<uint32_t>(256, std::max<uint32_t>(1, nedge));
+    const uint32_t tiles_e = (nedge + epb_e - 1) / epb_e;
+    {
+      PROF(KID_ACC_PART);
+      hipLaunchKernelGGL(k_accum_partial<FO>, dim3(nspec, tiles_e), dim3(256), red_lds, c->stream, g,
+                         st->meas_rows, d_perm, d_cb, d_status, epb_e, c->partials.u8(), d_pc, d_sid,
+                         e0, e1);
+    }
+    {
+      PROF(KID_ACC_SPEC);
+      hipLaunchKernelGGL(k_accum_spec<FO>, dim3(nspec, (e1 - e0 + 127) / 128), dim3(256), 0,
+                         c->stream, g, (uint32_t)n, st->meas_rows, d_sid, d_swb, d_wl,
+                         reinterpret_cast<const uint64_t*>(st->spec_lo.p), st->spec_cy.u8(),
+                         st->spec_nd, e0, e1, d_status, c->partials.u8());
+    }
   }
   {
     PROF(KID_ACC_MERGE);
@@ -563,6 +669,7 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
                        agg->share.u8(), reinterpret_cast<unsigned long long*>(agg->counts.p));
   }
   HIPCHK(hipGetLastError());
+  // The host vectors must outlive the async copies.
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -629,6 +736,7 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
   *out = nullptr;
   HIPCHK(hipSetDevice(device));
   auto* c = new prio3gpu_ctx();
+  if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
   c->device = device;
   memcpy(c->vk, verify_key, 16);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -721,7 +829,8 @@ int prio3gpu_state_destroy(prio3gpu_state* st) {
   if (!st) return 0;
   if (st->ctx) (void)hipStreamSynchronize(st->ctx->stream);
   for (DevBuf* b : {&st->t, &st->jr, &st->part, &st->seed, &st->meas, &st->proof, &st->prep,
-                    &st->msg, &st->status, &st->nonces, &st->pub, &st->input, &st->w})
+                    &st->msg, &st->status, &st->nonces, &st->pub, &st->input, &st->w,
+                    &st->spec_lo, &st->spec_cy})
     b->release();
   delete st;
   return 0;

@@ -278,6 +278,16 @@ __global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t ag
 // instructions (global_load_lds_dwordx4, 16 B/lane, ~6 rows per instruction instead of 64) while
 // block b is permuted.  All lanes of a wave take part in the fill, so lanes past n or with a
 // failed status still run the loop (on a clamped row) and just do not store.
+// lo:hi += x (64-bit), cy += carry out
+DEVI void acc_u64(uint32_t& lo, uint32_t& hi, uint32_t& cy, uint64_t x) {
+  asm("v_add_co_u32 %0, vcc, %0, %3\n\t"
+      "v_addc_co_u32 %1, vcc, %1, %4, vcc\n\t"
+      "v_addc_co_u32 %2, vcc, 0, %2, vcc"
+      : "+v"(lo), "+v"(hi), "+v"(cy)
+      : "v"((uint32_t)x), "v"((uint32_t)(x >> 32))
+      : "vcc");
+}
+
 constexpr uint32_t kJrWin = 176;  // bytes per report in the LDS window (22 words)
 constexpr uint32_t kJrWaveLds = 64 * kJrWin;
 
@@ -285,7 +295,8 @@ template <class FO>
 __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id, CRows nonces,
                                             CRows public_shares, CRows blinds, CRows meas,
                                             Rows out_part, Rows out_seed, Rows out_jr,
-                                            const uint8_t* status) {
+                                            const uint8_t* status, uint64_t* spec_lo,
+                                            uint8_t* spec_cy) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t r0w = blockIdx.x * blockDim.x + (tid & ~63u);  // first report of this wave
@@ -345,6 +356,38 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
         const uint64_t cur = L[w + 1];
         s[w] ^= (prev >> 48) | (cur << 16);
         prev = cur;
+      }
+      if (spec_lo != nullptr) {
+        // Speculative accumulation: column sums of the window's 21 new words over the wave's 64
+        // rows (lane = word wc + 21 gq, rows gq, gq+3, ...; lane 63's sums are never used), as a
+        // 64-bit sum plus carry count.  All reads of a half are issued before the adds.
+        const uint32_t wc = lane % 21u, gq = lane / 21u;
+        const uint8_t* colp = win + 8u * (1u + wc);
+        uint32_t l32 = 0, h32 = 0, cy = 0;
+#pragma unroll
+        for (int i0 = 0; i0 < 22; i0 += 11) {
+          uint64_t xs[11];
+#pragma unroll
+          for (int i = 0; i < 11; ++i) {
+            const uint32_t row = gq + 3u * (uint32_t)(i0 + i);
+            xs[i] = *reinterpret_cast<const uint64_t*>(colp + (row & 63u) * kJrWin);
+            if (i0 + i == 21 && row >= 64u) xs[i] = 0ull;
+          }
+#pragma unroll
+          for (int i = 0; i < 11; ++i) acc_u64(l32, h32, cy, xs[i]);
+        }
+        const uint32_t s1 = (lane + 21u) & 63u, s2 = (lane + 42u) & 63u;
+        const uint32_t la = __shfl(l32, (int)s1, 64), ha = __shfl(h32, (int)s1, 64);
+        const uint32_t ca = __shfl(cy, (int)s1, 64);
+        const uint32_t lb = __shfl(l32, (int)s2, 64), hb = __shfl(h32, (int)s2, 64);
+        const uint32_t cb = __shfl(cy, (int)s2, 64);
+        if (lane < 21u) {
+          acc_u64(l32, h32, cy, ((uint64_t)ha << 32) | la);
+          acc_u64(l32, h32, cy, ((uint64_t)hb << 32) | lb);
+          const size_t at = (size_t)(r0w >> 6) * (size_t)nd + (size_t)(21 * b - 5 + lane);
+          spec_lo[at] = ((uint64_t)h32 << 32) | l32;
+          spec_cy[at] = (uint8_t)(cy + ca + cb);
+        }
       }
     } else if (b == 0) {
 #pragma unroll
@@ -1189,15 +1232,19 @@ template <class FO>
 __global__ void __launch_bounds__(256) k_accum_partial(Cfg cfg, CRows meas, const uint32_t* perm,
                                                        const uint32_t* chunk_begin,
                                                        const uint8_t* status, uint32_t epb,
-                                                       uint8_t* partials, uint32_t* part_counts) {
+                                                       uint8_t* partials, uint32_t* part_counts,
+                                                       const uint32_t* chunk_ids, uint32_t e_head,
+                                                       uint32_t e_tail) {
   using T = typename FO::T;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   T* red = reinterpret_cast<T*>(smem);
-  const uint32_t ch = blockIdx.x;
+  const uint32_t ch = chunk_ids ? chunk_ids[blockIdx.x] : blockIdx.x;
   const uint32_t tid = threadIdx.x;
   const uint32_t G = blockDim.x / epb;
   const uint32_t el = tid % epb, g = tid / epb;
-  const uint32_t e = blockIdx.y * epb + el;
+  // logical element li -> measurement element: [0, e_head) then [e_tail, meas_len)
+  const uint32_t li = blockIdx.y * epb + el;
+  const uint32_t e = li < e_head ? li : e_tail + (li - e_head);
   const uint32_t b0 = chunk_begin[ch], b1 = chunk_begin[ch + 1];
   T acc = FO::zero();
   if (g < G && e < cfg.meas_len) {
@@ -1237,6 +1284,62 @@ __global__ void __launch_bounds__(256) k_accum_partial(Cfg cfg, CRows meas, cons
     if (cnt) atomicAdd(rc, cnt);
     __syncthreads();
     if (tid == 0) part_counts[ch] = *rc;
+  }
+}
+
+// Speculative chunks: the measurement-share words [2 e0, 2 e1) were column-summed per wave by
+// k_jr (spec_lo/spec_cy).  Sum them over the chunk's waves, subtract the rows that did not end
+// with status OK (and the clamped rows past n), and fold the two 64-bit word sums of element e into
+// one canonical element:  x = A + 2^64 B,  2^128 = 28 2^64 - 1 (mod p).  Thread pair (2t, 2t+1)
+// = the two words of element e0 + 128 blockIdx.y + t.
+template <class FO>
+__global__ void __launch_bounds__(256) k_accum_spec(Cfg cfg, uint32_t n, CRows meas,
+                                                    const uint32_t* chunk_ids,
+                                                    const uint32_t* chunk_wbegin,
+                                                    const uint32_t* waves, const uint64_t* spec_lo,
+                                                    const uint8_t* spec_cy, uint32_t nd,
+                                                    uint32_t e0, uint32_t e1,
+                                                    const uint8_t* status, uint8_t* partials) {
+  typedef unsigned __int128 u128;
+  const uint32_t ch = chunk_ids[blockIdx.x];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t e = e0 + blockIdx.y * 128u + (tid >> 1);
+  const uint32_t wd = 2u * e + (tid & 1u);
+  const bool act = e < e1;
+  u128 acc = 0;
+  const uint32_t wb = chunk_wbegin[blockIdx.x], we = chunk_wbegin[blockIdx.x + 1];
+  for (uint32_t q = wb; q < we; ++q) {
+    const uint32_t w = waves[q];
+    if (act) {
+      const size_t at = (size_t)w * nd + wd;
+      acc += (u128)spec_lo[at] + ((u128)spec_cy[at] << 64);
+    }
+    const uint32_t r = w * 64u + lane;
+    const bool fail = (r >= n) || status[r] != ST_OK;
+    uint64_t mask = __ballot(fail);
+    while (mask) {
+      const uint32_t i = (uint32_t)__builtin_ctzll(mask);
+      mask &= mask - 1ull;
+      const uint32_t rr = w * 64u + i < n ? w * 64u + i : n - 1u;
+      if (act) acc -= (u128)ld64(meas.at(rr) + (size_t)wd * 8u);
+    }
+  }
+  const uint64_t alo = (uint64_t)acc, ahi = (uint64_t)(acc >> 64);
+  const uint64_t blo = __shfl_xor(alo, 1, 64), bhi = __shfl_xor(ahi, 1, 64);
+  if (act && (tid & 1u) == 0u) {
+    // value = alo + 2^64 (ahi + blo) + 2^128 bhi
+    const u128 P = ((u128)0xFFFFFFFFFFFFFFFFull << 64) - ((u128)27ull << 64) + 1;  // 2^128-28*2^64+1
+    const u128 x1 = (u128)ahi + blo;                  // < 2^65
+    const u128 x2 = (u128)bhi + (uint64_t)(x1 >> 64);  // small
+    const u128 v = ((u128)(uint64_t)x1 << 64) | alo;   // < 2^128
+    const u128 k = (u128)(uint64_t)x2 * 28u;           // 2^128 x2 = x2 (28 2^64 - 1)
+    u128 t = v + (k << 64);
+    if (t < v) t += ((u128)28u << 64) - 1;              // carry out of 2^128
+    t -= (uint64_t)x2;                                  // no underflow: k << 64 >= x2
+    while (t >= P) t -= P;
+    uint8_t* dst = partials + ((size_t)ch * cfg.meas_len + e) * 16u;
+    st64(dst, (uint64_t)t);
+    st64(dst + 8, (uint64_t)(t >> 64));
   }
 }
 
