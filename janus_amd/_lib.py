@@ -13,6 +13,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 LIB_DIR = ROOT / "lib"
 LIB_PATH = LIB_DIR / "libprio3gpu.so"
+# Tuning experiments may point at another build of the same library (still the HIP engine).
+if os.environ.get("PRIO3GPU_LIB"):
+    LIB_PATH = Path(os.environ["PRIO3GPU_LIB"]).resolve()
 CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 

@@ -169,6 +169,7 @@ struct prio3gpu_ctx {
   DevBuf perm, chunks, partials, pcounts, spec_idx;
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
   bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
+  size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
 };
 
@@ -445,7 +446,8 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   if (g.jr_len > 0) {
     {
       PROF(KID_JR);
-      hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), (TPB / 64) * kJrWaveLds, c->stream, g, N,
+      const size_t jr_lds = std::max<size_t>((TPB / 64) * kJrWaveLds, std::min<size_t>(c->jr_lds, 160 * 1024));
+      hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), jr_lds, c->stream, g, N,
                          (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
                          Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status,
                          spec_lo, spec_cy);
@@ -737,6 +739,7 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
   HIPCHK(hipSetDevice(device));
   auto* c = new prio3gpu_ctx();
   if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
+  if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
   c->device = device;
   memcpy(c->vk, verify_key, 16);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

@@ -72,6 +72,12 @@ DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out);
 // One permutation per loop iteration (a single inlined Keccak-f per loop: ~35 KB of VOP3 code, so
 // two hot copies would not fit the instruction cache).  168-byte blocks alternate parity: even
 // blocks hold 10 whole elements + the low half of the next, odd blocks start with its high half.
+// Fast path: an element whose high 64 bits are below 2^64 - 28 is canonical (< p), which fails with
+// probability 28 / 2^64 per element; when every element of the block passes and all fit, they are
+// stored unconditionally at immediate offsets from one address.  Otherwise the block takes the
+// exact per-element path (prio's rejection sampling), so the output is the same either way.
+DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
+
 template <>
 DEVI void squeeze_vec<Field128Ops, 24>(uint64_t s[25], uint32_t n, uint8_t* out) {
   using FO = Field128Ops;
@@ -79,7 +85,31 @@ DEVI void squeeze_vec<Field128Ops, 24>(uint64_t s[25], uint32_t n, uint8_t* out)
   uint32_t parity = 0;
   uint64_t carry = 0;
   while (true) {
+    bool fast = cnt + 11u <= n;
     if (parity == 0) {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 1]);
+    } else {
+      fast &= hi_ok(s[0]);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
+    }
+    if (fast) {
+      uint64_t* o = reinterpret_cast<uint64_t*>(out + (size_t)cnt * 16);
+      if (parity == 0) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+          *reinterpret_cast<ulonglong2*>(o + 2 * k) = make_ulonglong2(s[2 * k], s[2 * k + 1]);
+        carry = s[20];
+        cnt += 10u;
+      } else {
+        *reinterpret_cast<ulonglong2*>(o) = make_ulonglong2(carry, s[0]);
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+          *reinterpret_cast<ulonglong2*>(o + 2 * k + 2) = make_ulonglong2(s[2 * k + 1], s[2 * k + 2]);
+        cnt += 11u;
+      }
+    } else if (parity == 0) {
 #pragma unroll
       for (int k = 0; k < 10; ++k) {
         F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
@@ -306,41 +336,39 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
   const uint32_t rr = r < n ? r : n - 1u;
   uint8_t* win = smem + (tid >> 6) * kJrWaveLds;
 
-  const uint8_t* nz = nonces.at(rr);
-  const uint8_t* bl = blinds.at(rr);
-  const uint64_t nonce_lo = ld64(nz), nonce_hi = ld64(nz + 8);
   const uint8_t* data = meas.at(rr);
   const uint32_t nbytes = cfg.meas_len * cfg.es;
-  MsgBlock pre;
-  pre.clear();
-  pre.header(cfg.algo_id, DST_JOINT_RAND_PART, ld64(bl), ld64(bl + 8));
-  pre.put8(25, agg_id);
-  pre.put64(26, nonce_lo);
-  pre.put64(34, nonce_hi);
   const int64_t nd = nbytes / 8;
   const int64_t total = 42 + (int64_t)nbytes;
   const int64_t nblocks = total / 168 + 1;
   const int64_t padw = total >> 3;
   const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
 
-  // LDS-DMA piece q of this lane: flat piece P = 64q + lane = (row, k) with 11 pieces per row
-  uint32_t voff[11];
-#pragma unroll
-  for (int q = 0; q < 11; ++q) {
-    const uint32_t P = 64u * q + lane;
-    const uint32_t row = P / 11u, k = P - row * 11u;
-    const uint32_t rowc = (r0w + row < n ? r0w + row : n - 1u) - r0w;
-    voff[q] = rowc * (uint32_t)meas.stride + 16u * k;
-  }
+  // LDS-DMA piece q of this lane: flat piece P = 64q + lane = (row, k) with 11 pieces per row.
+  // Recomputed per fill from lane = 11 la + lb (a few VALU ops per piece) instead of holding 11
+  // offsets live across the permutation: k_jr must stay <= 168 VGPRs (3 waves per SIMD).
+  const uint32_t la0 = lane / 11u, lb0 = lane - 11u * la0;
+  const uint32_t rlim = (n - r0w < 64u ? n - r0w : 64u) - 1u;  // last valid row of the wave
+  const uint32_t mstride = (uint32_t)meas.stride;
   const uint8_t* wbase = meas.base + (size_t)r0w * meas.stride;
   auto is_fast = [&](int64_t b) { return (b >= 1) && (21 * b + 15 < nd) && (21 * b + 20 < padw); };
   auto stage = [&](int64_t b) {  // window <- words [21b-6, 21b+16) of every row of the wave
     const uint8_t* src = wbase + 8 * (21 * b - 6);
+    // opaque copies: keep LICM from hoisting the 11 per-lane offsets out of the loop
+    uint32_t la, lb;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(la) : "v"(la0));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lb) : "v"(lb0));
 #pragma unroll
-    for (int q = 0; q < 11; ++q)
+    for (int q = 0; q < 11; ++q) {
+      const uint32_t cq = (64u * q) / 11u, dq = (64u * q) % 11u;  // 64q = 11 cq + dq
+      const uint32_t t = lb + dq;
+      const uint32_t wrap = t >= 11u ? 1u : 0u;
+      const uint32_t row = min(la + cq + wrap, rlim);
+      const uint32_t k = t - 11u * wrap;
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src + voff[q]),
+          (const __attribute__((address_space(1))) void*)(src + (row * mstride + 16u * k)),
           (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, 0, 0);
+    }
   };
 
   uint64_t s[25];
@@ -361,17 +389,22 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
         // Speculative accumulation: column sums of the window's 21 new words over the wave's 64
         // rows (lane = word wc + 21 gq, rows gq, gq+3, ...; lane 63's sums are never used), as a
         // 64-bit sum plus carry count.  All reads of a half are issued before the adds.
-        const uint32_t wc = lane % 21u, gq = lane / 21u;
-        const uint8_t* colp = win + 8u * (1u + wc);
+        const uint32_t gq = lane / 21u, wc = lane - 21u * gq;
+        // rows gq + 3i: one base address, the row steps are immediate offsets of ds_read_b64
+        const uint8_t* colp = win + 8u * (1u + wc) + gq * kJrWin;
         uint32_t l32 = 0, h32 = 0, cy = 0;
 #pragma unroll
         for (int i0 = 0; i0 < 22; i0 += 11) {
           uint64_t xs[11];
 #pragma unroll
           for (int i = 0; i < 11; ++i) {
-            const uint32_t row = gq + 3u * (uint32_t)(i0 + i);
-            xs[i] = *reinterpret_cast<const uint64_t*>(colp + (row & 63u) * kJrWin);
-            if (i0 + i == 21 && row >= 64u) xs[i] = 0ull;
+            const int ii = i0 + i;
+            if (ii < 21) {
+              xs[i] = *reinterpret_cast<const uint64_t*>(colp + 3u * (uint32_t)ii * kJrWin);
+            } else {  // row 63 exists only for gq == 0
+              xs[i] = *reinterpret_cast<const uint64_t*>(win + 8u * (1u + wc) + 63u * kJrWin);
+              if (gq != 0u) xs[i] = 0ull;
+            }
           }
 #pragma unroll
           for (int i = 0; i < 11; ++i) acc_u64(l32, h32, cy, xs[i]);
@@ -390,6 +423,16 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
         }
       }
     } else if (b == 0) {
+      // prefix [agg_id] || nonce, built here so none of it stays live across the loop
+      const uint8_t* nz = nonces.at(rr);
+      const uint8_t* bl = blinds.at(rr);
+      const uint64_t nonce_hi = ld64(nz + 8);
+      MsgBlock pre;
+      pre.clear();
+      pre.header(cfg.algo_id, DST_JOINT_RAND_PART, ld64(bl), ld64(bl + 8));
+      pre.put8(25, agg_id);
+      pre.put64(26, ld64(nz));
+      pre.put64(34, nonce_hi);
 #pragma unroll
       for (int w = 0; w < 21; ++w) {
         uint64_t v = (w < 5) ? pre.w[w] : jr_data_word(w, data, nd, nonce_hi);
@@ -400,8 +443,8 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
     } else {
 #pragma unroll
       for (int w = 0; w < 21; ++w) {
-        const int64_t g = 21 * b + w;
-        uint64_t v = jr_data_word(g, data, nd, nonce_hi);
+        const int64_t g = 21 * b + w;  // >= 21: the nonce word is never needed here
+        uint64_t v = jr_data_word(g, data, nd, 0ull);
         if (padw == g) v ^= padv;
         if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
         s[w] ^= v;

@@ -1,0 +1,20 @@
+#!/bin/bash
+# A/B timing of library variants on one GPU box (bench.py, no CPU baseline).
+#   tools/ab.sh TAG "label1:ENV=..;ENV2=.." "label2:..." ...
+set -uo pipefail
+TAG=$1; shift
+O=gpurun_out; mkdir -p $O
+for spec in "$@"; do
+  label=${spec%%:*}; envs=${spec#*:}
+  echo "== $label ($envs)"
+  env $(echo "$envs" | tr ';' ' ') timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --cpu-baseline 0 > $O/ab_${TAG}_$label.log 2>&1
+  rc=$?
+  python3 -c "
+import json,sys
+for l in open('$O/ab_${TAG}_$label.log'):
+    if l.startswith('{'):
+        d=json.loads(l); print(' value', d['value'], 'ms/step', d['ms_per_step']); print(' ', d['kernels_ms_per_step'])
+" || tail -3 $O/ab_${TAG}_$label.log
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0
