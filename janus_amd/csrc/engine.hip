@@ -318,17 +318,38 @@ int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_
   s.prep_msg = g.prep_msg_len;
   s.aggregate_share = g.out_len * es;
 
-  // twiddles: alpha_m^k (k < m) and 1/m at index m, Montgomery form
+  // twiddles (Montgomery form), 3m + 1 entries:
+  //   [0, m)        alpha_m^k
+  //   m             1/m
+  //   [m+1, 2m+1)   S_i = sum_{k=1..calls} alpha_m^(ik)   (gadget-output sum as a dot product)
+  //   [2m+1, 3m+1)  alpha_m^k / m                          (Lagrange weight scale)
   const u128 p = (es == 16) ? P128 : P64;
   const u128 R = (es == 16) ? (u128)0 - P128 /* 2^128 mod p */ : ((u128)1 << 64) % P64;
   const u128 alpha = powmod(7, (p - 1) / g.m, p);
-  std::vector<uint8_t> tw((size_t)(g.m + 1) * es);
-  u128 a = 1;
-  for (uint32_t k = 0; k <= g.m; ++k) {
-    u128 v = (k < g.m) ? a : (p - (p - 1) / g.m);
-    u128 mv = mulmod(v, R, p);
-    for (uint32_t b = 0; b < es; ++b) tw[(size_t)k * es + b] = (uint8_t)(mv >> (8 * b));
-    a = mulmod(a, alpha, p);
+  const u128 inv_m = p - (p - 1) / g.m;
+  std::vector<u128> tv(3 * (size_t)g.m + 1);
+  {
+    u128 a = 1;
+    for (uint32_t k = 0; k < g.m; ++k) {
+      tv[k] = a;
+      tv[2 * g.m + 1 + k] = mulmod(a, inv_m, p);
+      a = mulmod(a, alpha, p);
+    }
+    tv[g.m] = inv_m;
+    for (uint32_t i = 0; i < g.m; ++i) {
+      const u128 x = tv[i];  // alpha^i
+      u128 y = x, acc = 0;
+      for (uint32_t k = 1; k <= g.calls; ++k) {
+        acc = addmod(acc, y, p);
+        y = mulmod(y, x, p);
+      }
+      tv[g.m + 1 + i] = acc;
+    }
+  }
+  std::vector<uint8_t> tw(tv.size() * es);
+  for (size_t k = 0; k < tv.size(); ++k) {
+    const u128 mv = mulmod(tv[k], R, p);
+    for (uint32_t b = 0; b < es; ++b) tw[k * es + b] = (uint8_t)(mv >> (8 * b));
   }
   CHK(c->twiddles.ensure(tw.size()));
   HIPCHK(hipMemcpy(c->twiddles.p, tw.data(), tw.size(), hipMemcpyHostToDevice));

@@ -942,57 +942,45 @@ __global__ void __launch_bounds__(256) k_flp_weights(Cfg cfg, uint32_t n, CRows 
   const T tmm = shfl_T<FO>(tl, (int)(m & 63u));  // t^m for m < 64
   const bool tbad = FO::eq(m == 128 ? t128 : (m == 64 ? t64 : tmm), one);
 
-  // ---- gadget poly coefficients d = lane + 64q (q < 4), p(t) partial sums ----
-  T cd[4];
-  T pt = FO::zero();
+  // ---- gadget poly, coefficients d = lane + 64q (q < 4): p(t), and the sum of the gadget outputs
+  //      sum_{k=1..calls} p(alpha^k) = sum_d c_d S[d mod m] with S[i] = sum_{k=1..calls} alpha^(ik)
+  //      (host table: twiddle entries m+1 .. 2m) -- a dot product instead of a size-m NTT ----
+  T pt = FO::zero(), gsum = FO::zero();
   {
     T tp = tl;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t d = lane + 64u * q;
-      cd[q] = FO::zero();
       if (d < gp_len) {
-        cd[q] = FO::load(gp + (size_t)d * ES);
-        bad |= !FO::is_canonical(cd[q]);
-        pt = FO::add(pt, FO::mul(tp, cd[q]));
+        const T cd = FO::load(gp + (size_t)d * ES);
+        bad |= !FO::is_canonical(cd);
+        pt = FO::add(pt, FO::mul(tp, cd));
+        gsum = FO::add(gsum, FO::mul(ld_tw<FO>(cfg, m + 1u + (d & (m - 1u))), cd));
       }
       if (q < 3) tp = FO::mul(tp, t64);
     }
   }
   pt = wave_sum<FO>(pt);
+  gsum = wave_sum<FO>(gsum);
 
-  // ---- NTT inputs (natural order), position p = 64e + lane ----
-  T A[2], B[2];
+  // ---- NTT input (natural order), position p = 64e + lane: t^(m-1-p) ----
+  T A[2];
   {
     const T S = shfl_T<FO>(tl, (int)((m - 1u - lane) & 63u));  // t^((m-1-lane) mod 64)
     if (m == 128) {
       A[0] = FO::mul(S, t64);  // t^(127-lane)
       A[1] = S;                // t^(63-lane)
-      B[0] = FO::add(cd[0], cd[2]);
-      B[1] = FO::add(cd[1], cd[3]);
-    } else if (m == 64) {
-      A[0] = S;
-      A[1] = FO::zero();
-      B[0] = FO::add(cd[0], cd[1]);
-      B[1] = FO::zero();
-    } else {  // m < 64: fold c_(l+m) from lane l+m
-      const T up = shfl_T<FO>(cd[0], (int)((lane + m) & 63u));
+    } else {
       A[0] = lane < m ? S : FO::zero();
-      B[0] = lane < m ? (lane + m < gp_len ? FO::add(cd[0], up) : cd[0]) : FO::zero();
       A[1] = FO::zero();
-      B[1] = FO::zero();
     }
   }
-  // ---- DIF NTTs: X[k] = sum_i x_i alpha_m^(ik), output at bitrev position ----
+  // ---- DIF NTT: X[k] = sum_i x_i alpha_m^(ik), output at bitrev position ----
   if (m == 128) {
     const T w = ld_tw<FO>(cfg, lane);  // alpha_128^lane
-    T u = A[0], v = A[1];
+    const T u = A[0], v = A[1];
     A[0] = FO::add(u, v);
     A[1] = FO::mul(FO::sub(u, v), w);
-    u = B[0];
-    v = B[1];
-    B[0] = FO::add(u, v);
-    B[1] = FO::mul(FO::sub(u, v), w);
   }
   const uint32_t E = m == 128 ? 2u : 1u;
   for (uint32_t h = (m >= 64 ? 32u : m >> 1); h >= 1; h >>= 1) {
@@ -1001,31 +989,24 @@ __global__ void __launch_bounds__(256) k_flp_weights(Cfg cfg, uint32_t n, CRows 
 #pragma unroll
     for (uint32_t e = 0; e < 2; ++e) {
       if (e < E) {
-        const T oa = shfl_xor_T<FO>(A[e], (int)h), ob = shfl_xor_T<FO>(B[e], (int)h);
+        const T oa = shfl_xor_T<FO>(A[e], (int)h);
         const T sa = hi ? FO::sub(oa, A[e]) : FO::add(A[e], oa);
-        const T sb = hi ? FO::sub(ob, B[e]) : FO::add(B[e], ob);
         A[e] = hi ? FO::mul(sa, w) : sa;
-        B[e] = hi ? FO::mul(sb, w) : sb;
       }
     }
   }
-  // ---- Lagrange weights LM[k] = Y_k alpha^k / m, gadget outputs G[k] = B ----
-  const T inv_m = ld_tw<FO>(cfg, m);
+  // ---- Lagrange weights LM[k] = Y_k alpha^k / m (alpha^k / m: twiddle entries 2m+1 .. 3m) ----
   uint32_t K[2];
   T LMv[2];
-  T lsum = FO::zero(), gsum = FO::zero();
+  T lsum = FO::zero();
 #pragma unroll
   for (uint32_t e = 0; e < 2; ++e) {
     const uint32_t p = 64u * e + lane;
     K[e] = bitrev(p & (m - 1u), logm);
-    LMv[e] = FO::mul(FO::mul(A[e], ld_tw<FO>(cfg, K[e])), inv_m);
-    if (e < E && p < m && K[e] >= 1u && K[e] <= C) {
-      lsum = FO::add(lsum, LMv[e]);
-      gsum = FO::add(gsum, B[e]);
-    }
+    LMv[e] = FO::mul(A[e], ld_tw<FO>(cfg, 2u * m + 1u + K[e]));
+    if (e < E && p < m && K[e] >= 1u && K[e] <= C) lsum = FO::add(lsum, LMv[e]);
   }
   lsum = wave_sum<FO>(lsum);
-  gsum = wave_sum<FO>(gsum);
   const T l0 = shfl_T<FO>(LMv[0], 0);  // position 0 holds k = 0 (lane 0, e = 0)
 
   // ---- r powers: RP[j] = r^j,  rc = r^c,  MM[k] = LM[k] rc^(k-1) ----
@@ -1195,36 +1176,57 @@ __global__ void __launch_bounds__(256) k_flp_wires(Cfg cfg, uint32_t n, FlpDims 
 template <class FO>
 __global__ void __launch_bounds__(256) k_decide(Cfg cfg, uint32_t n, CRows leader_prep,
                                                 CRows helper_prep, Rows out_msg, uint8_t* status) {
+  // One wave per 64 reports: the wave walks its reports one at a time, reading the two verifier
+  // shares coalesced (lane i takes wire pairs i, i + 64, ...) and reducing G across the wave; lane q
+  // keeps report q's decision.  Then every lane derives its own report's prep msg (1 Keccak-f).
   using T = typename FO::T;
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  if (status[r] != ST_OK) return;
-  const uint8_t* a = leader_prep.at(r);
-  const uint8_t* b = helper_prep.at(r);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t r0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  if (r0 >= n) return;  // wave-uniform
+  const uint32_t nr = n - r0 < 64u ? n - r0 : 64u;
   const size_t ES = FO::ES;
-  bool bad = false;
-  auto vsum = [&](uint32_t i) -> T {
-    const T x = FO::load(a + i * ES), y = FO::load(b + i * ES);
-    bad |= !FO::is_canonical(x) || !FO::is_canonical(y);
-    return FO::add(x, y);
-  };
-  const T v = vsum(0);
-  T g = FO::zero();
-  if (cfg.kind == KIND_SUM) {
-    const T w = vsum(1);
-    g = FO::sub(FO::mul(FO::to_mont(w), w), w);
-  } else {
-    for (uint32_t j = 0; j < cfg.arity / 2; ++j) {
-      const T w0 = vsum(1 + 2 * j), w1 = vsum(2 + 2 * j);
-      g = FO::add(g, FO::mul(FO::to_mont(w0), w1));
+  const uint32_t npairs = cfg.kind == KIND_SUM ? 1u : cfg.arity / 2u;
+  bool mine = false;
+  for (uint32_t q = 0; q < nr; ++q) {
+    const uint32_t rq = r0 + q;
+    if (__builtin_amdgcn_readfirstlane(status[rq]) != ST_OK) continue;  // wave-uniform
+    const uint8_t* a = leader_prep.at(rq);
+    const uint8_t* b = helper_prep.at(rq);
+    bool bad = false;
+    T g = FO::zero();
+    for (uint32_t j = lane; j < npairs; j += 64u) {
+      if (cfg.kind == KIND_SUM) {  // PolyEval(x^2 - x) on the single wire
+        const T x = FO::load(a + ES), y = FO::load(b + ES);
+        bad |= !FO::is_canonical(x) || !FO::is_canonical(y);
+        const T w = FO::add(x, y);
+        g = FO::sub(FO::mul(FO::to_mont(w), w), w);
+      } else {  // Mul / ParallelSum(Mul): sum_j w_2j w_2j+1
+        const uint8_t* pa = a + (size_t)(1u + 2u * j) * ES;
+        const uint8_t* pb = b + (size_t)(1u + 2u * j) * ES;
+        const T x0 = FO::load(pa), x1 = FO::load(pa + ES);
+        const T y0 = FO::load(pb), y1 = FO::load(pb + ES);
+        bad |= !FO::is_canonical(x0) || !FO::is_canonical(x1) || !FO::is_canonical(y0) ||
+               !FO::is_canonical(y1);
+        g = FO::add(g, FO::mul(FO::to_mont(FO::add(x0, y0)), FO::add(x1, y1)));
+      }
     }
+    g = wave_sum<FO>(g);
+    const T va = FO::load(a), vb = FO::load(b);
+    const T pa = FO::load(a + (size_t)(1u + cfg.arity) * ES);
+    const T pb = FO::load(b + (size_t)(1u + cfg.arity) * ES);
+    bad |= !FO::is_canonical(va) || !FO::is_canonical(vb) || !FO::is_canonical(pa) ||
+           !FO::is_canonical(pb);
+    const bool ok = !__any(bad) && FO::is_zero(FO::add(va, vb)) && FO::eq(g, FO::add(pa, pb));
+    if (lane == q) mine = ok;
   }
-  const T pt = vsum(1 + cfg.arity);
-  bool ok = !bad && FO::is_zero(v) && FO::eq(g, pt);
-  if (!ok) {
+  const uint32_t r = r0 + lane;
+  if (r >= n || status[r] != ST_OK) return;
+  if (!mine) {
     status[r] = ST_VDAF_PREP_ERROR;
     return;
   }
+  const uint8_t* a = leader_prep.at(r);
+  const uint8_t* b = helper_prep.at(r);
   if (cfg.jr_len > 0) {
     const uint8_t* pa = a + (size_t)cfg.verifier_len * ES;
     const uint8_t* pb = b + (size_t)cfg.verifier_len * ES;
