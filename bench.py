@@ -19,6 +19,7 @@ import math
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -71,6 +72,10 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--workers", type=int, default=1,
+                    help="concurrent aggregation-job workers per GPU, one engine context (HIP "
+                         "stream) and one contiguous slice of the batch each (Janus "
+                         "max_concurrent_job_workers)")
     args = ap.parse_args()
 
     import torch
@@ -101,7 +106,10 @@ def main():
     import hashlib
     vk = hashlib.shake_128(b"verify-key" + cfg_id).digest(16)
 
-    vdaf = Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=local_rank)
+    W = max(1, args.workers)
+    vdafs = [Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=local_rank)
+             for _ in range(W)]
+    vdaf = vdafs[0]
     s = vdaf.sizes
 
     # ---- synthetic inputs: B distinct reports per rank (SURVEY §8(d) recipe).  The recipe's
@@ -137,39 +145,67 @@ def main():
     d_hst = torch.zeros(B, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
 
-    ls, hs = vdaf.new_state(0, B), vdaf.new_state(1, B)
-    # running aggregates (the batch aggregation); with N > 1 each step accumulates into per-GPU
-    # partials that the RCCL merge flushes into the totals
-    lagg, hagg = vdaf.new_aggregate(1), vdaf.new_aggregate(1)
-    lpart, hpart = (vdaf.new_aggregate(1), vdaf.new_aggregate(1)) if world > 1 else (lagg, hagg)
     comm = None
     if world > 1:
         uid = [Comm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = Comm(uid[0], world, rank, local_rank)
     L = lib()
-    ctx = vdaf._ctx
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    # W job workers, each with its own context (HIP stream), states and aggregates over a
+    # contiguous slice of the batch; running aggregates are the batch aggregation; with N > 1 each
+    # step accumulates into per-GPU partials that the RCCL merge flushes into the totals
+    class Worker:
+        pass
+
+    bounds = [B * w // W for w in range(W + 1)]
+    workers = []
+    for w in range(W):
+        wk = Worker()
+        wk.v, lo, hi = vdafs[w], bounds[w], bounds[w + 1]
+        wk.n = hi - lo
+        wk.ls, wk.hs = wk.v.new_state(0, wk.n), wk.v.new_state(1, wk.n)
+        wk.lagg, wk.hagg = wk.v.new_aggregate(1), wk.v.new_aggregate(1)
+        wk.lpart, wk.hpart = ((wk.v.new_aggregate(1), wk.v.new_aggregate(1)) if world > 1
+                              else (wk.lagg, wk.hagg))
+        sl = slice(lo, hi)
+        wk.p = dict(nonces=P(d_nonces[sl]), pub=P(d_pub[sl]) if d_pub is not None else None,
+                    lin=P(d_lin[sl]), hin=P(d_hin[sl]), lprep=P(d_lprep[sl]),
+                    msgs=P(d_msgs[sl]) if s.prep_msg else None, lst=P(d_lst[sl]),
+                    hst=P(d_hst[sl]))
+        workers.append(wk)
+
+    def run_worker(wk):
+        p, ctx = wk.p, wk.v._ctx
+        check(L.prio3gpu_prepare_init(ctx, wk.ls._h, wk.n, p["nonces"], p["pub"], p["lin"],
+                                      p["lprep"], p["lst"]), "leader prepare_init")
+        check(L.prio3gpu_helper_init(ctx, wk.hs._h, wk.n, p["nonces"], p["pub"], p["hin"],
+                                     p["lprep"], None, p["msgs"], p["hst"], wk.hpart._h),
+              "helper_init")
+        check(L.prio3gpu_prepare_next(ctx, wk.ls._h, wk.n, p["msgs"], p["lst"], None, None,
+                                      wk.lpart._h), "leader prepare_next")
+
+    pool = ThreadPoolExecutor(max_workers=W) if W > 1 else None
 
     def step():
         d_lst.zero_()
         d_hst.zero_()
         torch.cuda.synchronize()
-        check(L.prio3gpu_prepare_init(ctx, ls._h, B, P(d_nonces), P(d_pub), P(d_lin), P(d_lprep),
-                                      P(d_lst)), "leader prepare_init")
-        check(L.prio3gpu_helper_init(ctx, hs._h, B, P(d_nonces), P(d_pub), P(d_hin), P(d_lprep),
-                                     None, P(d_msgs) if s.prep_msg else None, P(d_hst),
-                                     hpart._h), "helper_init")
-        check(L.prio3gpu_prepare_next(ctx, ls._h, B, P(d_msgs) if s.prep_msg else None, P(d_lst),
-                                      None, None, lpart._h), "leader prepare_next")
+        if pool is None:
+            run_worker(workers[0])
+        else:
+            list(pool.map(run_worker, workers))
         if comm is not None:  # flush the per-GPU partials into the totals (RCCL + mod-p add)
-            comm.allreduce(vdaf, lpart, lagg)
-            comm.allreduce(vdaf, hpart, hagg)
+            for wk in workers:
+                comm.allreduce(wk.v, wk.lpart, wk.lagg)
+                comm.allreduce(wk.v, wk.hpart, wk.hagg)
 
     for _ in range(args.warmup):
         step()
-    check(L.prio3gpu_prof_enable(ctx, 1), "prof")
-    L.prio3gpu_prof_read(ctx, (ctypes.c_double * 16)(), (ctypes.c_uint64 * 16)(), 16)
+    for wk in workers:
+        check(L.prio3gpu_prof_enable(wk.v._ctx, 1), "prof")
+        L.prio3gpu_prof_read(wk.v._ctx, (ctypes.c_double * 16)(), (ctypes.c_uint64 * 16)(), 16)
 
     def barrier():
         torch.cuda.synchronize()
@@ -183,11 +219,17 @@ def main():
         step()
     barrier()
     elapsed = time.perf_counter() - t0
-    ms = (ctypes.c_double * 16)()
-    nl = (ctypes.c_uint64 * 16)()
-    nk = L.prio3gpu_prof_read(ctx, ms, nl, 16)
-    kt = {L.prio3gpu_prof_kernel_name(i).decode(): (ms[i], nl[i]) for i in range(nk) if nl[i]}
-    check(L.prio3gpu_prof_enable(ctx, 0), "prof")
+    kt = {}
+    for wk in workers:
+        ms = (ctypes.c_double * 16)()
+        nl = (ctypes.c_uint64 * 16)()
+        nk = L.prio3gpu_prof_read(wk.v._ctx, ms, nl, 16)
+        for i in range(nk):
+            if nl[i]:
+                name = L.prio3gpu_prof_kernel_name(i).decode()
+                a, b = kt.get(name, (0.0, 0))
+                kt[name] = (a + ms[i], b + nl[i])
+        check(L.prio3gpu_prof_enable(wk.v._ctx, 0), "prof")
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -196,8 +238,17 @@ def main():
     # ---- parity gate: statuses, counts, aggregate == plaintext sum (and == CPU restatement) ------
     assert int(d_lst.max().item()) == 0 and int(d_hst.max().item()) == 0, "rejected reports"
     total_steps = args.warmup + args.steps
-    la, lc = lagg.read(0)
-    ha, hc = hagg.read(0)
+    def total(attr):  # merge the workers' aggregates (mod p) and counts
+        acc, cnt = None, 0
+        for wk in workers:
+            a, c = getattr(wk, attr).read(0)
+            vec = vdaf.decode_field_vec(a)
+            acc = vec if acc is None else [(x + y) % vdaf.modulus for x, y in zip(acc, vec)]
+            cnt += c
+        return b"".join(int(x).to_bytes(s.field_size, "little") for x in acc), cnt
+
+    la, lc = total("lagg")
+    ha, hc = total("hagg")
     exp_count = total_steps * B * world
     assert lc == exp_count and hc == exp_count, (lc, hc, exp_count)
     meas = syn["meas"]
@@ -223,25 +274,26 @@ def main():
     dom = max(kt.items(), key=lambda kv: kv[1][0])
     dname, (dms, dlaunch) = dom
     avg_launch_s = dms / 1e3 / dlaunch
-    # B reports per launch; k_jr runs once per aggregator (2 launches per step)
+    # B / W reports per launch; k_jr runs once per aggregator and worker (2 W launches per step)
+    nlaunch = bounds[1] - bounds[0]
     if dname in perms and perms[dname]:
-        ops = perms[dname] * B * OPS_PER_PERM
+        ops = perms[dname] * nlaunch * OPS_PER_PERM
         achieved = ops / avg_launch_s / 1e12
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
                 "kernel": dname, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "model": f"{perms[dname]} Keccak-f[1600]/report x {OPS_PER_PERM} int32 ops "
-                         f"(SURVEY §8(d)) x {B} reports/launch"}
+                         f"(SURVEY §8(d)) x {nlaunch} reports/launch"}
     else:
         roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": None, "traffic": None, "kernel": dname,
                 "avg_launch_ms": round(avg_launch_s * 1e3, 3)}
     if dname in perms and perms[dname]:
-        perm_rate = perms[dname] * B / avg_launch_s
+        perm_rate = perms[dname] * nlaunch / avg_launch_s
         roof["keccak_perms_per_s"] = round(perm_rate, 1)
         roof["algorithmic_hbm_bytes_per_launch"] = (
-            B * s.meas_len * s.field_size if dname == "k_jr" else
-            B * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand" else None)
+            nlaunch * s.meas_len * s.field_size if dname == "k_jr" else
+            nlaunch * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand" else None)
     prof_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
     if os.path.exists(prof_path):  # PMC pass of the same command (tools/profile_round.sh)
         try:
@@ -298,8 +350,9 @@ def main():
         "dtype": "u128 (Field128 mod p)" if s.field_size == 16 else "u64 (Field64 mod p)",
         "data": f"synthetic: {B} distinct reports/GPU (SURVEY §8(d) recipe; shares made by the GPU "
                 f"client shard), resident in HBM",
-        "config": {"workload": label, "reports_per_gpu_per_step": B,
-                   "parallelism": f"report-sharded x{world}, RCCL all-gather merge"},
+        "config": {"workload": label, "reports_per_gpu_per_step": B, "job_workers_per_gpu": W,
+                   "parallelism": f"report-sharded x{world}, {W} job stream(s)/GPU, "
+                                  f"RCCL all-gather merge"},
         "roofline": roof,
         "cpu_baseline": cpu,
         "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
