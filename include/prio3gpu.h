@@ -55,7 +55,13 @@ enum prio3gpu_kind {
   PRIO3GPU_COUNT = 0,     /* Prio3Count                     Field64  */
   PRIO3GPU_SUM = 1,       /* Prio3Sum { bits }               Field128 */
   PRIO3GPU_SUMVEC = 2,    /* Prio3SumVec { bits, length, chunk_length }  Field128 */
-  PRIO3GPU_HISTOGRAM = 3  /* Prio3Histogram { length, chunk_length }     Field128 */
+  PRIO3GPU_HISTOGRAM = 3, /* Prio3Histogram { length, chunk_length }     Field128 */
+  /* Prio3FixedPoint{16,32,64}BitBoundedL2VecSum { length } (core/src/task.rs:24-59,
+   * aggregator.rs:839-861): bits = 16/32/64 (FixedI16<U15>/FixedI32<U31>/FixedI64<U63>),
+   * length = entries; chunk_length is ignored (prio picks both gadgets' chunk lengths with
+   * optimal_chunk_length).  Field128, algorithm ID 0xFFFF0000.  Measurements for prio3gpu_shard
+   * are not supported for this kind (clients shard on the CPU). */
+  PRIO3GPU_FPVEC = 4
 };
 
 enum prio3gpu_status {
@@ -93,7 +99,8 @@ typedef struct prio3gpu_sizes {
   uint32_t aggregate_share;     /* bytes: output_len * field_size */
 } prio3gpu_sizes;
 
-/* Prio3::new_{count,sum,sum_vec,histogram}(2, ...) + verify key (aggregator.rs:797-840).
+/* Prio3::new_{count,sum,sum_vec,histogram,fixedpoint_boundedl2_vec_sum}(2, ...) + verify key
+ * (aggregator.rs:797-861).
  * `bits`, `length`, `chunk_length` are ignored where the kind does not use them.
  * `device` = HIP device ordinal. */
 int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,

@@ -6,12 +6,14 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "../../include/prio3gpu.h"
 #include "prio3_kernels.h"
+#include "fpvec_kernels.h"
 
 using namespace p3g;
 
@@ -127,12 +129,13 @@ struct DevBuf {
 
 enum KernelId {
   KID_QUERY = 0, KID_EXPAND, KID_JR, KID_FLP, KID_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_MERGE,
-  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_FLP_WIRES, KID_ACC_SPEC, KID_COUNT
+  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_FLP_WIRES, KID_ACC_SPEC, KID_FPV_FINAL,
+  KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_jr", "k_flp_query", "k_decide", "k_prepare_next",
     "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge", "k_shard_*", "k_flp_prove",
-    "k_flp_wires", "k_accum_spec"};
+    "k_flp_wires", "k_accum_spec", "k_fpv_finalize"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -163,7 +166,7 @@ struct prio3gpu_ctx {
   uint8_t vk[16];
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf twiddles, twiddles2;
+  DevBuf twiddles, twiddles1, twiddles2;
   // generic staging (inputs given as host pointers) and scratch
   DevBuf io[6];
   DevBuf perm, chunks, partials, pcounts, spec_idx;
@@ -201,6 +204,7 @@ struct prio3gpu_state {
   size_t cap = 0;
   size_t n = 0;
   DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input, w;
+  DevBuf fpart, flags;  // FixedPointBoundedL2VecSum: wire partials per row group, query flags
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
   // speculative accumulation: per-wave column sums of meas-share words, written by k_jr
   DevBuf spec_lo, spec_cy;
@@ -224,10 +228,69 @@ struct prio3gpu_comm {
 
 namespace {
 
+// prio `optimal_chunk_length` (src/vdaf/prio3.rs, ext): among gadget_calls = 2^k - 1,
+// k = round(log2(len + 1)) .. 1, the chunk length minimising the ParallelSum(Mul) proof length
+// 2 chunk + 2 ((1 + calls).next_power_of_two() - 1) + 1; the first minimum (largest k) wins.
+uint32_t optimal_chunk_length(uint32_t len) {
+  if (len <= 1) return 1;
+  const int max_log2 = (int)std::lround(std::log2((double)len + 1.0));
+  uint64_t best_cost = ~0ull;
+  uint32_t best = 1;
+  for (int k = max_log2; k >= 1; --k) {
+    const uint64_t calls = (1ull << k) - 1;
+    const uint64_t chunk = (len + calls - 1) / calls;
+    const uint64_t cost = 2 * chunk + 2 * (next_pow2((uint32_t)(1 + calls)) - 1) + 1;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = (uint32_t)chunk;
+    }
+  }
+  return best;
+}
+
+// FLP tables of one gadget (Montgomery form), 3m + 1 entries:
+//   [0, m)        alpha_m^k
+//   m             1/m
+//   [m+1, 2m+1)   S_i = sum_{k=1..calls} alpha_m^(ik)   (gadget-output sum as a dot product)
+//   [2m+1, 3m+1)  alpha_m^k / m                          (Lagrange weight scale)
+int upload_tables(DevBuf& buf, uint32_t m, uint32_t calls, uint32_t es) {
+  const u128 p = (es == 16) ? P128 : P64;
+  const u128 R = (es == 16) ? (u128)0 - P128 /* 2^128 mod p */ : ((u128)1 << 64) % P64;
+  const u128 alpha = powmod(7, (p - 1) / m, p);
+  const u128 inv_m = p - (p - 1) / m;
+  std::vector<u128> tv(3 * (size_t)m + 1);
+  u128 a = 1;
+  for (uint32_t k = 0; k < m; ++k) {
+    tv[k] = a;
+    tv[2 * m + 1 + k] = mulmod(a, inv_m, p);
+    a = mulmod(a, alpha, p);
+  }
+  tv[m] = inv_m;
+  for (uint32_t i = 0; i < m; ++i) {
+    const u128 x = tv[i];  // alpha^i
+    u128 y = x, acc = 0;
+    for (uint32_t k = 1; k <= calls; ++k) {
+      acc = addmod(acc, y, p);
+      y = mulmod(y, x, p);
+    }
+    tv[m + 1 + i] = acc;
+  }
+  std::vector<uint8_t> tw(tv.size() * es);
+  for (size_t k = 0; k < tv.size(); ++k) {
+    const u128 mv = mulmod(tv[k], R, p);
+    for (uint32_t b = 0; b < es; ++b) tw[k * es + b] = (uint8_t)(mv >> (8 * b));
+  }
+  CHK(buf.ensure(tw.size()));
+  HIPCHK(hipMemcpy(buf.p, tw.data(), tw.size(), hipMemcpyHostToDevice));
+  return 0;
+}
+
 int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_t chunk) {
   Cfg& g = c->cfg;
   g.kind = (uint32_t)kind;
-  g.algo_id = (uint32_t)kind;  // Count 0, Sum 1, SumVec 2, Histogram 3 (VDAF-07 algorithm IDs)
+  // VDAF-07 algorithm IDs: Count 0, Sum 1, SumVec 2, Histogram 3; FixedPoint L2 0xFFFF0000
+  g.algo_id = kind == PRIO3GPU_FPVEC ? 0xFFFF0000u : (uint32_t)kind;
+  g.qr_len = kind == PRIO3GPU_FPVEC ? 2u : 1u;
   uint32_t calls = 0, arity = 0, prove_rand = 0;
   switch (kind) {
     case PRIO3GPU_COUNT:
@@ -278,13 +341,30 @@ int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_
       arity = 2 * chunk;
       prove_rand = 2 * chunk;
       break;
+    case PRIO3GPU_FPVEC:
+      if ((bits != 16 && bits != 32 && bits != 64) || length == 0) {
+        set_err("Prio3FixedPointBoundedL2VecSum: bits must be 16, 32 or 64 and length >= 1");
+        return PRIO3GPU_E_ARG;
+      }
+      g.es = 16;
+      g.meas_len = bits * length + 2 * bits - 2;  // entry bits || norm bits
+      g.out_len = length;
+      g.jr_len = 2;
+      chunk = optimal_chunk_length(g.meas_len);
+      calls = (g.meas_len + chunk - 1) / chunk;
+      arity = 2 * chunk;
+      g.chunk1 = optimal_chunk_length(length);
+      g.calls1 = (length + g.chunk1 - 1) / g.chunk1;
+      prove_rand = 2 * chunk + g.chunk1;
+      break;
     default:
       set_err("unknown kind %d", kind);
       return PRIO3GPU_E_ARG;
   }
   g.bits = bits;
   g.length = length;
-  g.chunk = (kind == PRIO3GPU_SUMVEC || kind == PRIO3GPU_HISTOGRAM) ? chunk : 0;
+  g.chunk =
+      (kind == PRIO3GPU_SUMVEC || kind == PRIO3GPU_HISTOGRAM || kind == PRIO3GPU_FPVEC) ? chunk : 0;
   g.calls = calls;
   g.arity = arity;
   g.prove_rand_len = prove_rand;
@@ -297,6 +377,20 @@ int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_
   g.gp_len = 2 * (g.m - 1) + 1;  // every gadget here has degree 2
   g.proof_len = arity + g.gp_len;
   g.verifier_len = 1 + arity + 1;
+  if (kind == PRIO3GPU_FPVEC) {
+    g.m1 = next_pow2(1 + g.calls1);
+    g.logm1 = ilog2(g.m1);
+    g.gp_len1 = 2 * (g.m1 - 1) + 1;
+    g.proof_len += g.chunk1 + g.gp_len1;
+    g.verifier_len += g.chunk1 + 1;
+    // k_fpv_weights keeps three m-entry tables and an r-power table in LDS
+    if (g.m > 2048 || g.chunk + 1 > 4096 ||
+        (size_t)16 * (3 * (size_t)g.m + g.chunk + 1 + 12) + 16 > 160 * 1024) {
+      set_err("FixedPointBoundedL2VecSum: length %u too large (m = %u, chunk = %u)", length, g.m,
+              g.chunk);
+      return PRIO3GPU_E_ARG;
+    }
+  }
   const uint32_t es = g.es;
   g.leader_share_len = es * (g.meas_len + g.proof_len) + (g.jr_len ? 16 : 0);
   g.helper_share_len = g.jr_len ? 48 : 32;
@@ -318,44 +412,17 @@ int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_
   s.prep_msg = g.prep_msg_len;
   s.aggregate_share = g.out_len * es;
 
-  // twiddles (Montgomery form), 3m + 1 entries:
-  //   [0, m)        alpha_m^k
-  //   m             1/m
-  //   [m+1, 2m+1)   S_i = sum_{k=1..calls} alpha_m^(ik)   (gadget-output sum as a dot product)
-  //   [2m+1, 3m+1)  alpha_m^k / m                          (Lagrange weight scale)
-  const u128 p = (es == 16) ? P128 : P64;
-  const u128 R = (es == 16) ? (u128)0 - P128 /* 2^128 mod p */ : ((u128)1 << 64) % P64;
-  const u128 alpha = powmod(7, (p - 1) / g.m, p);
-  const u128 inv_m = p - (p - 1) / g.m;
-  std::vector<u128> tv(3 * (size_t)g.m + 1);
-  {
-    u128 a = 1;
-    for (uint32_t k = 0; k < g.m; ++k) {
-      tv[k] = a;
-      tv[2 * g.m + 1 + k] = mulmod(a, inv_m, p);
-      a = mulmod(a, alpha, p);
-    }
-    tv[g.m] = inv_m;
-    for (uint32_t i = 0; i < g.m; ++i) {
-      const u128 x = tv[i];  // alpha^i
-      u128 y = x, acc = 0;
-      for (uint32_t k = 1; k <= g.calls; ++k) {
-        acc = addmod(acc, y, p);
-        y = mulmod(y, x, p);
-      }
-      tv[g.m + 1 + i] = acc;
-    }
-  }
-  std::vector<uint8_t> tw(tv.size() * es);
-  for (size_t k = 0; k < tv.size(); ++k) {
-    const u128 mv = mulmod(tv[k], R, p);
-    for (uint32_t b = 0; b < es; ++b) tw[k * es + b] = (uint8_t)(mv >> (8 * b));
-  }
-  CHK(c->twiddles.ensure(tw.size()));
-  HIPCHK(hipMemcpy(c->twiddles.p, tw.data(), tw.size(), hipMemcpyHostToDevice));
+  CHK(upload_tables(c->twiddles, g.m, g.calls, es));
   g.twiddles = c->twiddles.u8();
+  g.twiddles1 = nullptr;
+  if (kind == PRIO3GPU_FPVEC) {
+    CHK(upload_tables(c->twiddles1, g.m1, g.calls1, es));
+    g.twiddles1 = c->twiddles1.u8();
+  }
   // prover table: w^k (k < 2m, w = primitive 2m-th root), 1/m, 1/(2m); Montgomery
   {
+    const u128 p = (es == 16) ? P128 : P64;
+    const u128 R = (es == 16) ? (u128)0 - P128 /* 2^128 mod p */ : ((u128)1 << 64) % P64;
     const uint32_t m2 = 2 * g.m;
     const u128 w = powmod(7, (p - 1) / m2, p);
     std::vector<uint8_t> t2((size_t)(m2 + 2) * es);
@@ -413,6 +480,41 @@ bool spec_range(const Cfg& g, uint32_t& nd, uint32_t& e0, uint32_t& e1) {
   return e1 > e0;
 }
 
+// FixedPointBoundedL2VecSum FLP query (fpvec_kernels.h): weights, wire passes, finalize.
+int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, CRows proof,
+                     uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  const uint32_t N = (uint32_t)n;
+  const uint32_t H = fpv_rows(g);
+  const FpvW W = fpv_w_layout(g);
+  Rows wrows{st->w.u8(), (size_t)W.len * 16};
+  Rows prep{st->prep.u8(), g.prep_share_len};
+  uint32_t* flags = reinterpret_cast<uint32_t*>(st->flags.p);
+  HIPCHK(hipMemsetAsync(flags, 0, n * 4, c->stream));
+  const size_t lds = (size_t)16 * (3 * (size_t)g.m + g.chunk + 1 + 12) + 16;
+  {
+    PROF(KID_FLP);
+    hipLaunchKernelGGL(k_fpv_weights, dim3(N, 2), dim3(256), lds, c->stream, g, N, proof,
+                       CRows{st->t.u8(), 32}, CRows{st->jr.u8(), 32}, prep, d_status, wrows, flags);
+  }
+  {
+    PROF(KID_FLP_WIRES);
+    hipLaunchKernelGGL(k_fpv_wires0, dim3((g.chunk + 255) / 256, H, N), dim3(256), 0, c->stream, g,
+                       N, H, meas, CRows{wrows.base, wrows.stride}, d_status, st->fpart.u8(),
+                       flags);
+    hipLaunchKernelGGL(k_fpv_wires1, dim3((g.chunk1 + 255) / 256, N), dim3(256), 0, c->stream, g, N,
+                       meas, CRows{wrows.base, wrows.stride}, prep, d_status);
+  }
+  {
+    PROF(KID_FPV_FINAL);
+    hipLaunchKernelGGL(k_fpv_finalize, dim3((g.chunk + 255) / 256, N), dim3(256), 0, c->stream, g,
+                       N, H, meas, CRows{wrows.base, wrows.stride}, CRows{st->jr.u8(), 32},
+                       CRows{st->part.u8(), 16}, st->fpart.u8(), prep, d_status, flags);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 template <class FO>
 int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
                         const uint8_t* d_pub, const uint8_t* d_in, uint8_t* d_status) {
@@ -425,7 +527,7 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   memcpy(&vk_hi, c->vk + 8, 8);
   CRows nonces{d_nonces, 16};
   CRows pub{d_pub, g.public_share_len};
-  Rows t_rows{st->t.u8(), 16};
+  Rows t_rows{st->t.u8(), (size_t)16 * g.qr_len};
   {
     PROF(KID_QUERY);
     hipLaunchKernelGGL(k_query_rand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N, vk_lo, vk_hi,
@@ -472,6 +574,14 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
                          (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
                          Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status,
                          spec_lo, spec_cy);
+    }
+  }
+  if constexpr (FO::ES == 16) {
+    if (g.kind == KIND_FPVEC) {
+      CHK(launch_fpv_query(c, st, n, meas, proof, d_status));
+      st->meas_rows = meas;
+      st->n = n;
+      return 0;
     }
   }
   // FLP query: block per report.  ParallelSum types (SumVec, Histogram) split it in two: the
@@ -542,6 +652,14 @@ template <class FO>
 int launch_decide(prio3gpu_ctx* c, size_t n, const uint8_t* d_l, const uint8_t* d_h,
                   uint8_t* d_msg, uint8_t* d_status) {
   const Cfg& g = c->cfg;
+  if (g.kind == KIND_FPVEC) {
+    PROF(KID_DECIDE);
+    hipLaunchKernelGGL(k_fpv_decide, dim3((unsigned)n), dim3(256), 0, c->stream, g, (uint32_t)n,
+                       CRows{d_l, g.prep_share_len}, CRows{d_h, g.prep_share_len},
+                       Rows{d_msg, g.prep_msg_len}, d_status);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   {
     PROF(KID_DECIDE);
     hipLaunchKernelGGL(k_decide<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, (uint32_t)n,
@@ -686,7 +804,8 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
   }
   {
     PROF(KID_ACC_MERGE);
-    const uint32_t bpe = (g.kind == KIND_SUMVEC || g.kind == KIND_SUM) ? g.bits : 1u;
+    const uint32_t bpe =
+        (g.kind == KIND_SUMVEC || g.kind == KIND_SUM || g.kind == KIND_FPVEC) ? g.bits : 1u;
     hipLaunchKernelGGL(k_accum_merge<FO>, grid1(g.out_len, 256 / bpe), dim3(256), 0, c->stream, g, nch,
                        d_cs, c->partials.u8(), reinterpret_cast<const uint32_t*>(c->pcounts.p),
                        agg->share.u8(), reinterpret_cast<unsigned long long*>(agg->counts.p));
@@ -783,6 +902,7 @@ int prio3gpu_ctx_destroy(prio3gpu_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->twiddles.release();
+  c->twiddles1.release();
   c->twiddles2.release();
   for (auto& b : c->io) b.release();
   c->perm.release();
@@ -828,7 +948,7 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   const Cfg& g = c->cfg;
   const size_t N = capacity;
   int rc = 0;
-  rc |= st->t.ensure(N * 16);
+  rc |= st->t.ensure(N * 16 * g.qr_len);
   rc |= st->jr.ensure(N * 16 * std::max<uint32_t>(1, g.jr_len));
   rc |= st->part.ensure(N * 16);
   rc |= st->seed.ensure(N * 16);
@@ -837,6 +957,11 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   rc |= st->status.ensure(N);
   if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM)
     rc |= st->w.ensure(N * (size_t)flp_w_len(g) * g.es);
+  if (g.kind == KIND_FPVEC) {
+    rc |= st->w.ensure(N * (size_t)fpv_w_layout(g).len * 16);
+    rc |= st->fpart.ensure(N * (size_t)fpv_rows(g) * g.chunk * 32);
+    rc |= st->flags.ensure(N * 4);
+  }
   if (agg_id == 1) {
     rc |= st->meas.ensure(N * (size_t)g.meas_len * g.es);
     rc |= st->proof.ensure(N * (size_t)g.proof_len * g.es);
@@ -1194,6 +1319,10 @@ int prio3gpu_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t*
   if (!nonces || !measurements || !rand || !out_leader || !out_helper ||
       (c->cfg.jr_len && !out_public)) {
     set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  if (c->cfg.kind == KIND_FPVEC) {
+    set_err("shard: FixedPointBoundedL2VecSum clients are not batched on the GPU");
     return PRIO3GPU_E_ARG;
   }
   HIPCHK(hipSetDevice(c->device));

@@ -1,0 +1,338 @@
+// FLP query + decide for Prio3FixedPointBoundedL2VecSum (prio 0.15.1
+// src/flp/types/fixedpoint_l2.rs, ext; Janus VdafInstance::Prio3FixedPoint{16,32,64}BitBoundedL2VecSum,
+// aggregator/src/aggregator.rs:839-861, dispatched at :1115-1145).
+//
+// The type's circuit has TWO gadgets (restated in oracle/prio3.py FixedPointBoundedL2VecSum):
+//   gadget 0 = ParallelSum(Mul, c0) range check over all bits x_0..x_{L0-1}
+//              (L0 = n*entries + 2n-2; parallel_sum_range_checks on jr[0]),
+//   gadget 1 = ParallelSum(PolyEval([2^(2n-2), -2^n, 1]), c1) over the decoded entries
+//              z_e = sum_l 2^l x_{ne+l}  (padding: the share of the encoded zero, 2^(n-1)/2),
+//   v = jr[1] * sum_k p0(alpha0^k) + jr[1]^2 * (sum_k p1(alpha1^k) - sum_l 2^l x_{n entries + l}).
+// The verifier share is [v, wires0 (2 c0), p0(t0), wires1 (c1), p1(t1)] and decide checks
+// v == 0, G0(wires0) == p0(t0), G1(wires1) == p1(t1).
+//
+// Shapes are large and reports few (entries = 100k: 1.6M-element shares, 25.6 MB per report), so
+// unlike the ParallelSum kernels for SumVec (a wave per report), every step here spreads ONE
+// report over many blocks:
+//   k_fpv_weights   block per (report, gadget): power tables, one size-m NTT for the Lagrange
+//                   weights at t_g, gadget-output sum as a dot product with the host S table, p(t)
+//   k_fpv_wires0    block per (report, 256 columns, row group): lazily reduced dot products
+//                   sum_k (L_k r^(c(k-1))) x and sum_k L_k x over the measurement share (HBM stream)
+//   k_fpv_wires1    block per (report, 256 columns): decode z_e on the fly, sum_k L_k z
+//   k_fpv_finalize  block per (report, 256 columns): fold the row groups, v, p(t), joint-rand part
+//   k_fpv_decide    block per report
+#pragma once
+#include "prio3_kernels.h"
+
+namespace p3g {
+
+// Per-report weight row ("W"), element offsets (Field128 elements).
+struct FpvW {
+  uint32_t mm, lm, rp, b0, b1, g0, l1, c1, g1, len;
+};
+__host__ __device__ inline FpvW fpv_w_layout(const Cfg& g) {
+  FpvW w;
+  w.mm = 0;                       // L_k r^(c0 (k-1)), k = 1..calls0     (Montgomery)
+  w.lm = w.mm + g.calls;          // L_k, k = 1..calls0                  (Montgomery)
+  w.rp = w.lm + g.calls;          // r^(j+1), j < c0                     (Montgomery)
+  w.b0 = w.rp + g.chunk;          // L_0 s_2j                            (canonical)
+  w.b1 = w.b0 + g.chunk;          // L_0 s_2j+1 - (1/2) sum_k L_k        (canonical)
+  w.g0 = w.b1 + g.chunk;          // sum_k p0(alpha0^k)                  (canonical)
+  w.l1 = w.g0 + 1;                // L'_k, k = 1..calls1                 (Montgomery)
+  w.c1 = w.l1 + g.calls1;         // L'_0 s'_j + [padded] L'_calls1 z0   (canonical)
+  w.g1 = w.c1 + g.chunk1;         // sum_k p1(alpha1^k)                  (canonical)
+  w.len = w.g1 + 1;
+  return w;
+}
+
+// Row groups of k_fpv_wires0 (calls split H ways so one report fills many blocks).
+__host__ __device__ inline uint32_t fpv_rows(const Cfg& g) { return g.calls < 32u ? g.calls : 32u; }
+
+// Flag bits per report (OR-ed by every kernel of the query, turned into a status by finalize).
+enum : uint32_t { FPV_BAD_ENCODING = 1u, FPV_ROOT_OF_UNITY = 2u };
+
+// One in-place radix-2 DIT NTT of size m (input bit-reversed) in LDS, twiddles `tw` (Montgomery).
+DEVI void ntt1_lds(F128* A, uint32_t m, uint32_t logm, const uint8_t* tw, uint32_t tid,
+                   uint32_t nthr) {
+  using FO = Field128Ops;
+  for (uint32_t st = 1; st <= logm; ++st) {
+    const uint32_t half = 1u << (st - 1);
+    for (uint32_t q = tid; q < (m >> 1); q += nthr) {
+      const uint32_t grp = q >> (st - 1), k = q & (half - 1u);
+      const uint32_t i = grp * 2u * half + k, j = i + half;
+      const F128 w = FO::load(tw + (size_t)(k << (logm - st)) * 16u);
+      const F128 u = A[i];
+      const F128 v = FO::mul(w, A[j]);
+      A[i] = FO::add(u, v);
+      A[j] = FO::sub(u, v);
+    }
+    __syncthreads();
+  }
+}
+
+// grid (n, 2), 256 threads.  LDS: TP[m] | NA[m] | RC[m] | RP[c0+1] | RED[3*4] | flag
+__global__ void __launch_bounds__(256) k_fpv_weights(Cfg cfg, uint32_t n, CRows proof, CRows tq,
+                                                     CRows jr, Rows prep, const uint8_t* status,
+                                                     Rows wrows, uint32_t* flags) {
+  using FO = Field128Ops;
+  using T = F128;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t r = blockIdx.x, gi = blockIdx.y;
+  if (r >= n || status[r] != ST_OK) return;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t m = gi ? cfg.m1 : cfg.m, logm = gi ? cfg.logm1 : cfg.logm;
+  const uint32_t calls = gi ? cfg.calls1 : cfg.calls, c = gi ? cfg.chunk1 : cfg.chunk;
+  const uint32_t arity = gi ? cfg.chunk1 : cfg.arity, gp_len = gi ? cfg.gp_len1 : cfg.gp_len;
+  const uint8_t* tw = gi ? cfg.twiddles1 : cfg.twiddles;
+  const size_t ES = 16;
+  const FpvW W = fpv_w_layout(cfg);
+  T* TP = reinterpret_cast<T*>(smem);
+  T* NA = TP + m;
+  T* RC = NA + m;
+  T* RP = RC + m;
+  T* RED = RP + (cfg.chunk + 1);
+  uint32_t* flag = reinterpret_cast<uint32_t*>(RED + 12);
+  if (tid == 0) *flag = 0u;
+
+  // proof block of this gadget: [seeds (arity)] || [gadget poly (gp_len)]
+  const uint8_t* pr = proof.at(r) + (gi ? (size_t)(cfg.arity + cfg.gp_len) * ES : 0);
+  const T tm = FO::to_mont(FO::load(tq.at(r) + (size_t)gi * ES));
+  const T rm = FO::to_mont(FO::load(jr.at(r)));  // jr[0]: the range check's joint randomness
+  if (wave == 0) wave_pow_table<FO>(TP, tm, m, lane);
+  if (gi == 0 && wave == 1) wave_pow_table<FO>(RP, rm, c + 1, lane);
+  if (gi == 0 && wave == 2) wave_pow_table<FO>(RC, mont_pow<FO>(rm, c), calls, lane);
+  __syncthreads();
+  const T tmm = FO::mul(TP[m - 1], tm);  // t^m (Montgomery)
+  if (tid == 0 && FO::eq(tmm, FO::one_mont())) atomicOr(flag, FPV_ROOT_OF_UNITY);
+  for (uint32_t i = tid; i < m; i += nthr) NA[bitrev(i, logm)] = TP[m - 1 - i];
+  __syncthreads();
+  ntt1_lds(NA, m, logm, tw, tid, nthr);
+  // Lagrange weights L_k(t) = NTT(t^(m-1-i))[k] * alpha^k / m (table entry 2m+1+k), Montgomery.
+  uint8_t* wr = wrows.at(r);
+  T lsum = FO::zero();
+  for (uint32_t k = tid; k <= calls; k += nthr) {
+    const T L = FO::mul(NA[k], FO::load(tw + (size_t)(2 * m + 1 + k) * ES));
+    NA[k] = L;
+    if (k >= 1) {
+      lsum = FO::add(lsum, L);
+      if (gi == 0) {
+        FO::store(wr + (size_t)(W.mm + k - 1) * ES, FO::mul(L, RC[k - 1]));
+        FO::store(wr + (size_t)(W.lm + k - 1) * ES, L);
+      } else {
+        FO::store(wr + (size_t)(W.l1 + k - 1) * ES, L);
+      }
+    }
+  }
+  // p(t) = sum_{d<m} c_d t^d + t^m sum_{d>=m} c_d t^(d-m);  gsum = sum_d c_d S[d mod m]
+  bool bad = false;
+  T plo = FO::zero(), phi = FO::zero(), gsum = FO::zero();
+  for (uint32_t d = tid; d < gp_len; d += nthr) {
+    const T cd = FO::load(pr + (size_t)(arity + d) * ES);
+    bad |= !FO::is_canonical(cd);
+    const uint32_t dm = d & (m - 1u);
+    if (d < m) plo = FO::add(plo, FO::mul(TP[dm], cd));
+    else phi = FO::add(phi, FO::mul(TP[dm], cd));
+    gsum = FO::add(gsum, FO::mul(FO::load(tw + (size_t)(m + 1 + dm) * ES), cd));
+  }
+  T hsum = FO::zero();
+  block_sum3<FO>(plo, phi, gsum, RED, tid, nthr);
+  block_sum3<FO>(lsum, hsum, hsum, RED, tid, nthr);  // also orders the NA[k] = L writes
+  const T L0 = NA[0], Lc = NA[calls];
+  uint8_t* outp = prep.at(r);
+  if (gi == 0) {
+    const T half_l = FO::mul(lsum, FO::half());
+    for (uint32_t j = tid; j < c; j += nthr) {
+      const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
+      const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
+      bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
+      FO::store(wr + (size_t)(W.rp + j) * ES, RP[j + 1]);
+      FO::store(wr + (size_t)(W.b0 + j) * ES, FO::mul(L0, s0));
+      FO::store(wr + (size_t)(W.b1 + j) * ES, FO::sub(FO::mul(L0, s1), half_l));
+    }
+  } else {
+    // padded slots of the last call hold the share of the encoded zero: 2^(n-1) / 2 = 2^(n-2)
+    const uint32_t rem = cfg.length - (calls - 1) * c;
+    const uint32_t zb = cfg.bits - 2;
+    const T z0 = FO::from_u64x2(zb < 64 ? 1ull << zb : 0ull, zb >= 64 ? 1ull << (zb - 64) : 0ull);
+    const T pad = FO::mul(Lc, z0);
+    for (uint32_t j = tid; j < c; j += nthr) {
+      const T s = FO::load(pr + (size_t)j * ES);
+      bad |= !FO::is_canonical(s);
+      T v = FO::mul(L0, s);
+      if (j >= rem) v = FO::add(v, pad);
+      FO::store(wr + (size_t)(W.c1 + j) * ES, v);
+    }
+  }
+  if (bad) atomicOr(flag, FPV_BAD_ENCODING);
+  __syncthreads();
+  if (tid == 0) {
+    const T pt = FO::add(plo, FO::mul(tmm, phi));
+    FO::store(wr + (size_t)(gi ? W.g1 : W.g0) * ES, gsum);
+    const size_t pt_at = gi ? (size_t)(1 + cfg.arity + 1 + cfg.chunk1) : (size_t)(1 + cfg.arity);
+    FO::store(outp + pt_at * ES, pt);
+    if (*flag) atomicOr(&flags[r], *flag);
+  }
+}
+
+// grid (ceil(c0/256), H, n), 256 threads: thread = column j, block row group h: calls k = 1+h+qH.
+// part[(r*H + h)*c0 + j] = (sum_k MM_k x_idx, sum_k LM_k x_idx), idx = (k-1) c0 + j.
+__global__ void __launch_bounds__(256) k_fpv_wires0(Cfg cfg, uint32_t n, uint32_t H, CRows meas,
+                                                    CRows wrows, const uint8_t* status,
+                                                    uint8_t* part, uint32_t* flags) {
+  using FO = Field128Ops;
+  const uint32_t r = blockIdx.z, h = blockIdx.y;
+  if (r >= n || status[r] != ST_OK) return;
+  const uint32_t c = cfg.chunk;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= c) return;
+  const FpvW W = fpv_w_layout(cfg);
+  const uint8_t* xr = meas.at(r);
+  const uint8_t* wr = wrows.at(r);
+  Wide wa, wb;
+  wide_zero(wa);
+  wide_zero(wb);
+  bool bad = false;
+  for (uint32_t k = 1 + h; k <= cfg.calls; k += H) {
+    const uint32_t idx = (k - 1) * c + j;
+    if (idx >= cfg.meas_len) break;  // only the last call is partial
+    const F128 x = FO::load(xr + (size_t)idx * 16u);
+    bad |= !FO::is_canonical(x);
+    wide_mac(wa, FO::load(wr + (size_t)(W.mm + k - 1) * 16u), x);
+    wide_mac(wb, FO::load(wr + (size_t)(W.lm + k - 1) * 16u), x);
+  }
+  uint8_t* dst = part + (((size_t)r * H + h) * c + j) * 32u;
+  FO::store(dst, wide_reduce(wa));
+  FO::store(dst + 16, wide_reduce(wb));
+  if (bad) atomicOr(&flags[r], FPV_BAD_ENCODING);
+}
+
+// grid (ceil(c1/256), n), 256 threads: wire1_j = C1[j] + sum_k L'_k z_((k-1) c1 + j), z decoded
+// from the n bits of the entry (Horner from the top bit, mod p).
+__global__ void __launch_bounds__(256) k_fpv_wires1(Cfg cfg, uint32_t n, CRows meas, CRows wrows,
+                                                    Rows prep, const uint8_t* status) {
+  using FO = Field128Ops;
+  const uint32_t r = blockIdx.y;
+  if (r >= n || status[r] != ST_OK) return;
+  const uint32_t c = cfg.chunk1, nb = cfg.bits;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= c) return;
+  const FpvW W = fpv_w_layout(cfg);
+  const uint8_t* xr = meas.at(r);
+  const uint8_t* wr = wrows.at(r);
+  Wide acc;
+  wide_zero(acc);
+  for (uint32_t k = 1; k <= cfg.calls1; ++k) {
+    const uint32_t e = (k - 1) * c + j;
+    if (e >= cfg.length) break;
+    const uint8_t* xe = xr + (size_t)e * nb * 16u;
+    F128 z = FO::zero();
+    for (int l = (int)nb - 1; l >= 0; --l) z = FO::add(FO::dbl(z), FO::load(xe + (size_t)l * 16u));
+    wide_mac(acc, FO::load(wr + (size_t)(W.l1 + k - 1) * 16u), z);
+  }
+  const F128 w = FO::add(FO::load(wr + (size_t)(W.c1 + j) * 16u), wide_reduce(acc));
+  FO::store(prep.at(r) + (size_t)(1 + cfg.arity + 1 + j) * 16u, w);
+}
+
+// grid (ceil(c0/256), n), 256 threads: wires0 from the row-group partials; block x = 0 also writes
+// v, the joint-rand part and the report's status.
+__global__ void __launch_bounds__(256) k_fpv_finalize(Cfg cfg, uint32_t n, uint32_t H, CRows meas,
+                                                      CRows wrows, CRows jr, CRows part_in,
+                                                      const uint8_t* part, Rows prep,
+                                                      uint8_t* status, const uint32_t* flags) {
+  using FO = Field128Ops;
+  const uint32_t r = blockIdx.y;
+  if (r >= n || status[r] != ST_OK) return;
+  const uint32_t c = cfg.chunk;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const FpvW W = fpv_w_layout(cfg);
+  const uint8_t* wr = wrows.at(r);
+  uint8_t* outp = prep.at(r);
+  if (j < c) {
+    F128 a = FO::zero(), b = FO::zero();
+    for (uint32_t h = 0; h < H; ++h) {
+      const uint8_t* src = part + (((size_t)r * H + h) * c + j) * 32u;
+      a = FO::add(a, FO::load(src));
+      b = FO::add(b, FO::load(src + 16));
+    }
+    const F128 w0 = FO::add(FO::load(wr + (size_t)(W.b0 + j) * 16u),
+                            FO::mul(FO::load(wr + (size_t)(W.rp + j) * 16u), a));
+    const F128 w1 = FO::add(FO::load(wr + (size_t)(W.b1 + j) * 16u), b);
+    FO::store(outp + (size_t)(1 + 2 * j) * 16u, w0);
+    FO::store(outp + (size_t)(2 + 2 * j) * 16u, w1);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // submitted norm = sum_l 2^l x_(n entries + l), l < 2n - 2
+    const uint8_t* xn = meas.at(r) + (size_t)cfg.bits * cfg.length * 16u;
+    F128 sn = FO::zero();
+    for (int l = (int)(2 * cfg.bits - 3); l >= 0; --l)
+      sn = FO::add(FO::dbl(sn), FO::load(xn + (size_t)l * 16u));
+    const F128 r1 = FO::to_mont(FO::load(jr.at(r) + 16));
+    const F128 norm_check = FO::sub(FO::load(wr + (size_t)W.g1 * 16u), sn);
+    const F128 v = FO::add(FO::mul(r1, FO::load(wr + (size_t)W.g0 * 16u)),
+                           FO::mul(FO::mul(r1, r1), norm_check));
+    FO::store(outp, v);
+    const uint8_t* pp = part_in.at(r);
+    uint8_t* dst = outp + (size_t)cfg.verifier_len * 16u;
+    st64(dst, ld64(pp));
+    st64(dst + 8, ld64(pp + 8));
+    const uint32_t f = flags[r];
+    if (f & FPV_BAD_ENCODING) status[r] = ST_INVALID_MESSAGE;
+    else if (f & FPV_ROOT_OF_UNITY) status[r] = ST_VDAF_PREP_ERROR;
+  }
+}
+
+// prepare_shares_to_prepare_message for FixedPointBoundedL2VecSum: block per report.
+//   G0 = sum_j w_2j w_2j+1 (ParallelSum(Mul)),  G1 = sum_j (w_j^2 - 2^n w_j + 2^(2n-2)).
+__global__ void __launch_bounds__(256) k_fpv_decide(Cfg cfg, uint32_t n, CRows leader_prep,
+                                                    CRows helper_prep, Rows out_msg,
+                                                    uint8_t* status) {
+  using FO = Field128Ops;
+  using T = F128;
+  __shared__ T red[12];
+  __shared__ uint32_t sbad;
+  const uint32_t r = blockIdx.x;
+  if (r >= n || status[r] != ST_OK) return;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
+  if (tid == 0) sbad = 0u;
+  __syncthreads();
+  const uint8_t* a = leader_prep.at(r);
+  const uint8_t* b = helper_prep.at(r);
+  const uint32_t nb = cfg.bits;
+  // 2^n (Montgomery) and 2^(2n-2) (canonical)
+  const T k1 = FO::to_mont(FO::from_u64x2(nb < 64 ? 1ull << nb : 0ull, nb >= 64 ? 1ull : 0ull));
+  const uint32_t e2 = 2 * nb - 2;
+  const T k0 = FO::from_u64x2(e2 < 64 ? 1ull << e2 : 0ull, e2 >= 64 ? 1ull << (e2 - 64) : 0ull);
+  bool bad = false;
+  auto wire = [&](uint32_t i) {
+    const T x = FO::load(a + (size_t)i * 16u), y = FO::load(b + (size_t)i * 16u);
+    bad |= !FO::is_canonical(x) || !FO::is_canonical(y);
+    return FO::add(x, y);
+  };
+  T g0 = FO::zero(), g1 = FO::zero(), z = FO::zero();
+  for (uint32_t j = tid; j < cfg.chunk; j += nthr) {
+    const T w0 = wire(1 + 2 * j), w1 = wire(2 + 2 * j);
+    g0 = FO::add(g0, FO::mul(FO::to_mont(w0), w1));
+  }
+  const uint32_t base1 = 1 + cfg.arity + 1;
+  for (uint32_t j = tid; j < cfg.chunk1; j += nthr) {
+    const T w = wire(base1 + j);
+    g1 = FO::add(g1, FO::add(FO::sub(FO::mul(FO::to_mont(w), w), FO::mul(k1, w)), k0));
+  }
+  if (bad) atomicOr(&sbad, 1u);
+  block_sum3<FO>(g0, g1, z, red, tid, nthr);
+  if (tid != 0) return;
+  const T v = wire(0), p0 = wire(1 + cfg.arity), p1 = wire(base1 + cfg.chunk1);
+  const bool ok = !sbad && !bad && FO::is_zero(v) && FO::eq(g0, p0) && FO::eq(g1, p1);
+  if (!ok) {
+    status[r] = ST_VDAF_PREP_ERROR;
+    return;
+  }
+  const uint8_t* pa = a + (size_t)cfg.verifier_len * 16u;
+  const uint8_t* pb = b + (size_t)cfg.verifier_len * 16u;
+  uint64_t lo, hi;
+  derive_jr_seed(cfg.algo_id, ld64(pa), ld64(pa + 8), ld64(pb), ld64(pb + 8), lo, hi);
+  st64(out_msg.at(r), lo);
+  st64(out_msg.at(r) + 8, hi);
+}
+
+}  // namespace p3g

@@ -24,7 +24,13 @@
 
 namespace p3g {
 
-enum Kind : uint32_t { KIND_COUNT = 0, KIND_SUM = 1, KIND_SUMVEC = 2, KIND_HISTOGRAM = 3 };
+enum Kind : uint32_t {
+  KIND_COUNT = 0,
+  KIND_SUM = 1,
+  KIND_SUMVEC = 2,
+  KIND_HISTOGRAM = 3,
+  KIND_FPVEC = 4  // FixedPointBoundedL2VecSum (bits = 16/32/64 per entry, length = entries)
+};
 
 // Per-report status codes = DAP PrepareError (messages/src/lib.rs:2288-2298) + 0 = ok.
 enum Status : uint8_t { ST_OK = 0, ST_VDAF_PREP_ERROR = 5, ST_INVALID_MESSAGE = 8, ST_SKIPPED = 0xFF };
@@ -44,7 +50,11 @@ struct Cfg {
   uint32_t meas_len, proof_len, verifier_len, jr_len, out_len, prove_rand_len;
   uint32_t bits, length, chunk, calls, m, logm, arity, gp_len;
   uint32_t leader_share_len, helper_share_len, public_share_len, prep_share_len, prep_msg_len;
+  uint32_t qr_len;          // query-randomness elements (one per gadget)
   const uint8_t* twiddles;  // device: alpha_m^k, k < m, Montgomery form, ES bytes each
+  // FixedPointBoundedL2VecSum's second gadget, ParallelSum(PolyEval(norm poly), chunk1)
+  uint32_t chunk1, calls1, m1, logm1, gp_len1;
+  const uint8_t* twiddles1;  // same table layout as `twiddles`, for m1 / calls1
 };
 
 // A per-report byte array: element r at base + r*stride.
@@ -281,7 +291,7 @@ __global__ void __launch_bounds__(256) k_query_rand(Cfg cfg, uint32_t n, uint64_
   m.pad(41);
   uint64_t s[25];
   sponge_one_block<24>(s, m);
-  squeeze_vec<FO, 24>(s, 1, out_t.at(r));
+  squeeze_vec<FO, 24>(s, cfg.qr_len, out_t.at(r));
 }
 
 // Helper share expansion: meas share XOF(k_meas, dst1, [agg_id]) and proof share
@@ -1255,7 +1265,7 @@ __global__ void __launch_bounds__(256) k_prepare_next(Cfg cfg, uint32_t n, CRows
 template <class FO>
 DEVI typename FO::T out_elem(const Cfg& cfg, const uint8_t* x, uint32_t e) {
   using T = typename FO::T;
-  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_SUM) {
+  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_SUM || cfg.kind == KIND_FPVEC) {
     // sum_b 2^b x_b over `bits` consecutive elements, Horner from the top bit
     const uint8_t* p = x + (size_t)e * cfg.bits * FO::ES;
     T acc = FO::zero();
@@ -1400,7 +1410,8 @@ __global__ void __launch_bounds__(256) k_accum_merge(Cfg cfg, uint32_t nchunks,
                                                      unsigned long long* counts) {
   using T = typename FO::T;
   __shared__ T sums[256];
-  const uint32_t bpe = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_SUM) ? cfg.bits : 1u;
+  const uint32_t bpe =
+      (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_SUM || cfg.kind == KIND_FPVEC) ? cfg.bits : 1u;
   const uint32_t opb = 256 / bpe;  // output elements per block
   const uint32_t tid = threadIdx.x;
   const uint32_t o = blockIdx.x * opb + tid / bpe, b = tid % bpe;

@@ -2,8 +2,9 @@
 batched over whole aggregation jobs and executed by the MI355X HIP engine (libprio3gpu.so).
 
 Reference surface:
-  * `Prio3::new_count / new_sum / new_sum_vec / new_histogram` as constructed by Janus at
-    `aggregator/src/aggregator.rs:797-840`; chunk length = floor(sqrt(len)) (`core/src/task.rs:84-86`).
+  * `Prio3::new_count / new_sum / new_sum_vec / new_histogram /
+    new_fixedpoint_boundedl2_vec_sum` as constructed by Janus at
+    `aggregator/src/aggregator.rs:797-861`; chunk length = floor(sqrt(len)) (`core/src/task.rs:84-86`).
   * `Aggregator::prepare_init`, `prepare_shares_to_prepare_message`, `prepare_next`, `aggregate`
     (fake-VDAF mirror: `core/src/test_util/dummy_vdaf.rs:80-141`).
   * `Aggregatable::merge` (`dummy_vdaf.rs:230-242`), `Collector::unshard` (`collector/src/lib.rs:539`).
@@ -25,7 +26,7 @@ import numpy as np
 
 from ._lib import Prio3GpuError, check, lib
 
-COUNT, SUM, SUMVEC, HISTOGRAM = 0, 1, 2, 3
+COUNT, SUM, SUMVEC, HISTOGRAM, FPVEC = 0, 1, 2, 3, 4
 STATUS_OK, STATUS_VDAF_PREP_ERROR, STATUS_INVALID_MESSAGE = 0, 5, 8
 
 FIELD64_MODULUS = 2**64 - 2**32 + 1
@@ -180,6 +181,12 @@ class Prio3Gpu:
     def new_histogram(cls, length, chunk_length, verify_key, device=0):
         return cls(HISTOGRAM, verify_key, length=length, chunk_length=chunk_length, device=device)
 
+    @classmethod
+    def new_fixedpoint_boundedl2_vec_sum(cls, bits, length, verify_key, device=0):
+        """Janus `Prio3FixedPoint{16,32,64}BitBoundedL2VecSum { length }` (aggregator.rs:839-861):
+        `Prio3::new_fixedpoint_boundedl2_vec_sum_multithreaded(2, length)` over FixedI{bits}."""
+        return cls(FPVEC, verify_key, bits=bits, length=length, device=device)
+
     def close(self):
         if getattr(self, "_ctx", None):
             lib().prio3gpu_ctx_destroy(self._ctx)
@@ -301,13 +308,19 @@ class Prio3Gpu:
         es = self.sizes.field_size
         return [int.from_bytes(b[i:i + es], "little") for i in range(0, len(b), es)]
 
-    def unshard(self, aggregate_shares: Sequence[bytes]):
-        """`Collector::unshard`: sum the two aggregate shares and decode the result."""
+    def unshard(self, aggregate_shares: Sequence[bytes], num_measurements: int = None):
+        """`Collector::unshard` (collector/src/lib.rs:539): sum the aggregate shares and decode the
+        result.  Fixed-point vectors decode each sum d of `num_measurements` encoded entries as
+        d * 2^(1-bits) - num_measurements (prio `to_float_bits`)."""
         p = self.modulus
         vecs = [self.decode_field_vec(a) for a in aggregate_shares]
         out = [sum(col) % p for col in zip(*vecs)]
         if self.kind in (COUNT, SUM):
             return out[0]
+        if self.kind == FPVEC:
+            if num_measurements is None:
+                raise ValueError("fixed-point unshard needs the report count")
+            return [float(d) * 2.0 ** (1 - self.bits) - num_measurements for d in out]
         return out
 
 

@@ -284,6 +284,54 @@ class ParallelSumMul:
         return intt(fld, acc, n)[:2 * m - 1]
 
 
+class ParallelSumPolyEval:
+    """prio `ParallelSum<F, PolyEval<F>>` (and `...Multithreaded`): arity chunk, degree
+    len(poly)-1; G(x_0..x_{c-1}) = sum_j poly(x_j)."""
+
+    def __init__(self, poly: Sequence[int], chunk: int, calls: int):
+        self.poly = list(poly)
+        self.chunk = chunk
+        self.ARITY, self.DEGREE, self.CALLS = chunk, len(poly) - 1, calls
+
+    def eval(self, fld, inp):
+        p = fld.MODULUS
+        cs = [c % p for c in self.poly]
+        return sum(poly_eval(fld, cs, x) for x in inp) % p
+
+    def eval_poly(self, fld, polys):
+        # Every wire poly evaluated at n >= DEGREE*(m-1)+1 points, poly applied pointwise, summed,
+        # interpolated (the result is the unique polynomial of that degree).
+        p = fld.MODULUS
+        m = len(polys[0])
+        want = self.DEGREE * (m - 1) + 1
+        n = next_pow2(want)
+        cs = [c % p for c in self.poly]
+        acc = [0] * n
+        for j in range(self.chunk):
+            fv = ntt(fld, polys[j], n)
+            for i in range(n):
+                acc[i] = (acc[i] + poly_eval(fld, cs, fv[i])) % p
+        return intt(fld, acc, n)[:want]
+
+
+def optimal_chunk_length(measurement_length: int) -> int:
+    """prio `optimal_chunk_length` (src/vdaf/prio3.rs): among gadget_calls = 2^k - 1 (k = 1 ..
+    round(log2(len+1))), the chunk length minimising the ParallelSum(Mul) proof length
+    2*chunk + 2*((1 + calls).next_power_of_two() - 1) + 1 (first minimum from the largest k)."""
+    if measurement_length <= 1:
+        return 1
+    import math
+    max_log2 = round(math.log2(measurement_length + 1))
+    best = None
+    for log2 in range(max_log2, 0, -1):
+        calls = (1 << log2) - 1
+        chunk = (measurement_length + calls - 1) // calls
+        cost = 2 * chunk + 2 * (next_pow2(1 + calls) - 1) + 1
+        if best is None or cost < best[0]:
+            best = (cost, chunk)
+    return best[1]
+
+
 # ---------------------------------------------------------------------------------------------
 # Validity circuits (prio src/flp/types.rs, VDAF-07 §7.4)
 # ---------------------------------------------------------------------------------------------
@@ -451,6 +499,97 @@ class Histogram:
         return list(agg)
 
 
+def decode_bitvector(fld, bits: Sequence[int]) -> int:
+    """prio `decode_bitvector`: sum_l 2^l x_l (mod p)."""
+    p = fld.MODULUS
+    return sum((1 << l) * x for l, x in enumerate(bits)) % p
+
+
+class FixedPointBoundedL2VecSum:
+    """prio `FixedPointBoundedL2VecSum<FixedI{16,32,64}<U{15,31,63}>, ParallelSum<PolyEval>,
+    ParallelSum<Mul>>` (prio src/flp/types/fixedpoint_l2.rs, feature `experimental`), as
+    instantiated by Janus for `Prio3FixedPoint{16,32,64}BitBoundedL2VecSum { length }`
+    (`aggregator/src/aggregator.rs:839-861`, `Prio3::new_fixedpoint_boundedl2_vec_sum_multithreaded
+    (2, length)`).  Recalled structure (confidence M):
+      * entry x (fixed point, n bits, value in [-1, 1)) -> integer z = bits(x) + 2^(n-1) in
+        [0, 2^n), encoded as n LE bits; then the squared L2 norm of the integer entries
+        sum_e (z_e - 2^(n-1))^2 (< 2^(2n-2), i.e. norm < 1) as 2n-2 LE bits;
+      * gadget 0 = ParallelSum(Mul, c0): range check of all n*entries + 2n-2 bits with
+        `parallel_sum_range_checks` on joint_rand[0];
+      * gadget 1 = ParallelSum(PolyEval([2^(2n-2), -2^n, 1]), c1) over the decoded entries (padding
+        = share of the encoded zero 2^(n-1)/num_shares) = computed norm;
+      * valid = jr[1] * range + jr[1]^2 * (computed norm - submitted norm);
+      * c0 = optimal_chunk_length(n*entries + 2n-2), c1 = optimal_chunk_length(entries);
+      * truncate = decoded entries; decode_result(d, c) = d * 2^(1-n) - c  (to_float_bits).
+    Measurements are the fixed-point values' raw two's-complement integers (x * 2^(n-1))."""
+    ID = 0xFFFF0000
+    Field = Field128
+
+    def __init__(self, bits: int, entries: int):
+        assert bits in (16, 32, 64) and entries >= 1
+        self.bits, self.entries = bits, entries
+        self.bits_for_norm = 2 * bits - 2
+        self.range_norm_begin = bits * entries
+        self.range_norm_end = bits * entries + self.bits_for_norm
+        self.MEAS_LEN = self.range_norm_end
+        self.OUTPUT_LEN = entries
+        self.JOINT_RAND_LEN = 2
+        self.QUERY_RAND_LEN = 2
+        self.chunk0 = optimal_chunk_length(self.range_norm_end)
+        self.calls0 = (self.range_norm_end + self.chunk0 - 1) // self.chunk0
+        self.chunk1 = optimal_chunk_length(entries)
+        self.calls1 = (entries + self.chunk1 - 1) // self.chunk1
+        one = 1 << (bits - 1)
+        self.norm_summand_poly = [one * one, -2 * one, 1]
+        self.gadgets = [ParallelSumMul(self.chunk0, self.calls0),
+                        ParallelSumPolyEval(self.norm_summand_poly, self.chunk1, self.calls1)]
+        self.PROVE_RAND_LEN = 2 * self.chunk0 + self.chunk1
+
+    def encode(self, m: Sequence[int]) -> List[int]:
+        assert len(m) == self.entries
+        n = self.bits
+        out = []
+        norm = 0
+        for v in m:
+            assert -(1 << (n - 1)) <= v < (1 << (n - 1))
+            z = v + (1 << (n - 1))
+            out += [(z >> l) & 1 for l in range(n)]
+            norm += v * v
+        if norm >= 1 << self.bits_for_norm:
+            raise ValueError("measurement L2 norm exceeds 1")
+        out += [(norm >> l) & 1 for l in range(self.bits_for_norm)]
+        return out
+
+    def valid(self, g, meas, joint_rand, num_shares):
+        fld = self.Field
+        p = fld.MODULUS
+        range_check = parallel_sum_range_checks(fld, g[0], self.calls0,
+                                                meas[:self.range_norm_end], joint_rand[0],
+                                                self.chunk0, num_shares)
+        n = self.bits
+        decoded = [decode_bitvector(fld, meas[e * n:(e + 1) * n]) for e in range(self.entries)]
+        zero_share = (1 << (n - 1)) * fld.inv(num_shares) % p
+        computed = 0
+        c1 = self.chunk1
+        for i in range(0, self.entries, c1):
+            chunk = decoded[i:i + c1]
+            chunk = chunk + [zero_share] * (c1 - len(chunk))
+            computed = (computed + g[1](chunk)) % p
+        submitted = decode_bitvector(fld, meas[self.range_norm_begin:self.range_norm_end])
+        norm_check = (computed - submitted) % p
+        r = joint_rand[1]
+        return (r * range_check + r * r % p * norm_check) % p
+
+    def truncate(self, meas):
+        n = self.bits
+        return [decode_bitvector(self.Field, meas[e * n:(e + 1) * n]) for e in range(self.entries)]
+
+    def decode_result(self, agg, num_measurements: int = None):
+        """prio `CompatibleFloat::to_float` -> to_float_bits(d, c, n) = d * 2^(1-n) - c."""
+        assert num_measurements is not None, "FixedPoint decode needs the report count"
+        return [float(d) * 2.0 ** (1 - self.bits) - num_measurements for d in agg]
+
+
 # ---------------------------------------------------------------------------------------------
 # FLP (prio src/flp.rs: Type::prove / query / decide with ProveShimGadget / QueryShimGadget)
 # ---------------------------------------------------------------------------------------------
@@ -602,6 +741,11 @@ class Prio3:
     def new_histogram(cls, length, chunk_length):
         return cls(Histogram(length, chunk_length))
 
+    @classmethod
+    def new_fixedpoint_boundedl2_vec_sum(cls, bits, entries):
+        """Janus `VdafInstance::Prio3FixedPoint{16,32,64}BitBoundedL2VecSum { length }`."""
+        return cls(FixedPointBoundedL2VecSum(bits, entries))
+
     def dst(self, usage):
         return domain_separation_tag(self.typ.ID, usage)
 
@@ -739,8 +883,13 @@ class Prio3:
             agg = [(x + y) % p for x, y in zip(agg, o)]
         return agg
 
-    def unshard(self, agg_shares):
-        return self.typ.decode_result(self.aggregate(agg_shares))
+    def unshard(self, agg_shares, num_measurements: int = None):
+        """Collector::unshard (collector/src/lib.rs:539): decode_result(sum of shares); the
+        fixed-point type also needs the report count (prio to_float_bits)."""
+        agg = self.aggregate(agg_shares)
+        if isinstance(self.typ, FixedPointBoundedL2VecSum):
+            return self.typ.decode_result(agg, num_measurements)
+        return self.typ.decode_result(agg)
 
     # -- codecs (prio `Encode` impls; Janus decodes with (vdaf, agg_id) at aggregator.rs:1738) ---
     def encode_input_share(self, s: InputShare) -> bytes:
@@ -834,15 +983,33 @@ def synth_measurement(vdaf: Prio3, stream: bytes):
         nb = (typ.bits + 7) // 8
         return [int.from_bytes(stream[i * nb:(i + 1) * nb], "little") % (1 << typ.bits)
                 for i in range(typ.length)]
+    if isinstance(typ, FixedPointBoundedL2VecSum):
+        return synth_fixedpoint(typ.bits, typ.entries, stream)
     raise TypeError(typ)
+
+
+def synth_fixedpoint(bits: int, entries: int, stream: bytes) -> List[int]:
+    """x_j = u_j / sqrt(entries), u_j uniform in [-1, 1], quantized:
+    integer entries uniform in [-B, B] with entries * B^2 <= (2^(n-1) - 1)^2, so the L2 norm < 1.
+    8 stream bytes per entry."""
+    import math
+    one = (1 << (bits - 1)) - 1
+    B = math.isqrt(one * one // entries)
+    return [int.from_bytes(stream[8 * j:8 * j + 8], "little") % (2 * B + 1) - B
+            for j in range(entries)]
+
+
+def synth_meas_bytes(typ) -> int:
+    if isinstance(typ, SumVec):
+        return typ.length * ((typ.bits + 7) // 8)
+    if isinstance(typ, FixedPointBoundedL2VecSum):
+        return 8 * typ.entries
+    return 8
 
 
 def synth_report(vdaf: Prio3, cfg_id: bytes, i: int):
     """(nonce, measurement, rand) for report i; nonce = first 16 bytes of the stream."""
-    typ = vdaf.typ
-    meas_bytes = 8
-    if isinstance(typ, SumVec):
-        meas_bytes = typ.length * ((typ.bits + 7) // 8)
+    meas_bytes = synth_meas_bytes(vdaf.typ)
     total = 16 + vdaf.random_size() + meas_bytes
     s = synth_report_rand(cfg_id, i, total)
     nonce = s[:16]

@@ -19,7 +19,8 @@ from tests.reports import CONFIGS  # noqa: E402
 from oracle import prio3 as O  # noqa: E402
 
 SETS = [("count", 4), ("sum8", 3), ("sum32", 2), ("sumvec_small", 3), ("countvec15", 2),
-        ("hist4", 3), ("hist256", 2), ("sumvec_8_1000", 1)]
+        ("hist4", 3), ("hist256", 2), ("sumvec_8_1000", 1), ("fp16_3", 3), ("fp32_5", 2),
+        ("fp64_4", 2)]
 FIELDS = ["public_share", "leader_input_share", "helper_input_share", "leader_prep_share",
           "helper_prep_share", "prep_msg", "leader_out_share", "helper_out_share"]
 
@@ -53,7 +54,7 @@ def main():
             "reports": reports,
             "leader_agg_share": enc(v.fld.encode_vec(v.aggregate(lo))),
             "helper_agg_share": enc(v.fld.encode_vec(v.aggregate(ho))),
-            "unsharded": v.unshard([v.aggregate(lo), v.aggregate(ho)]),
+            "unsharded": v.unshard([v.aggregate(lo), v.aggregate(ho)], n),
         })
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "prio3_transcripts.json")
     with open(path, "w") as f:

@@ -27,6 +27,17 @@ CONFIGS = {
     "hist4": dict(kind=3, ctor=lambda: O.Prio3.new_histogram(4, 2), bits=0, length=4, chunk=2),
     "hist256": dict(kind=3, ctor=lambda: O.Prio3.new_histogram(256, 16), bits=0, length=256,
                     chunk=16),
+    # FixedPointBoundedL2VecSum (Janus Prio3FixedPoint{16,32,64}BitBoundedL2VecSum { length })
+    "fp16_3": dict(kind=4, ctor=lambda: O.Prio3.new_fixedpoint_boundedl2_vec_sum(16, 3), bits=16,
+                   length=3, chunk=0),
+    "fp32_5": dict(kind=4, ctor=lambda: O.Prio3.new_fixedpoint_boundedl2_vec_sum(32, 5), bits=32,
+                   length=5, chunk=0),
+    "fp64_4": dict(kind=4, ctor=lambda: O.Prio3.new_fixedpoint_boundedl2_vec_sum(64, 4), bits=64,
+                   length=4, chunk=0),
+    "fp16_300": dict(kind=4, ctor=lambda: O.Prio3.new_fixedpoint_boundedl2_vec_sum(16, 300),
+                     bits=16, length=300, chunk=0),
+    "fp16_5000": dict(kind=4, ctor=lambda: O.Prio3.new_fixedpoint_boundedl2_vec_sum(16, 5000),
+                      bits=16, length=5000, chunk=0),
 }
 
 
@@ -111,9 +122,13 @@ def expected_aggregate(b: Batch, which: str, mask=None, slots=None, slot=0) -> b
 
 def plaintext_sum(b: Batch, mask=None):
     """What unshard(aggregate) must equal (integration_tests/tests/common/mod.rs:225-398)."""
-    from oracle.prio3 import Count, Histogram, Sum, SumVec
+    from oracle.prio3 import Count, FixedPointBoundedL2VecSum, Histogram, Sum, SumVec
     typ = b.vdaf.typ
     ms = [m for r, m in enumerate(b.measurements) if mask is None or mask[r]]
+    if isinstance(typ, FixedPointBoundedL2VecSum):
+        # exact: sum of the fixed-point values (integers / 2^(bits-1)) as floats
+        sums = [sum(col) for col in zip(*ms)] if ms else [0] * typ.entries
+        return [s * 2.0 ** (1 - typ.bits) for s in sums]
     if isinstance(typ, (Count, Sum)):
         return sum(ms)
     if isinstance(typ, SumVec):

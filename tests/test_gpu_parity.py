@@ -13,7 +13,9 @@ from tests.reports import CONFIGS, expected_aggregate, make_batch, plaintext_sum
 pytestmark = pytest.mark.gpu
 
 SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
-         "hist256": 24, "sumvec_8_1000": 6}
+         "hist256": 24, "sumvec_8_1000": 6, "fp16_3": 12, "fp32_5": 8, "fp64_4": 8, "fp16_300": 6,
+         "fp16_5000": 2}
+FPVEC = [k for k in SIZES if k.startswith("fp")]
 
 _cache = {}
 
@@ -74,10 +76,13 @@ def test_aggregate_and_unshard(name):
     assert lc == hc == b.n
     assert la == expected_aggregate(b, "leader")[0]
     assert ha == expected_aggregate(b, "helper")[0]
-    assert v.unshard([la, ha]) == plaintext_sum(b)
+    if name in FPVEC:
+        assert v.unshard([la, ha], lc) == pytest.approx(plaintext_sum(b), rel=1e-12, abs=1e-12)
+    else:
+        assert v.unshard([la, ha]) == plaintext_sum(b)
 
 
-@pytest.mark.parametrize("name", ["sum8", "hist4", "sumvec_small", "count"])
+@pytest.mark.parametrize("name", ["sum8", "hist4", "sumvec_small", "count", "fp16_300"])
 def test_batch_slots_segmentation(name):
     b = batch(name)
     v = gpu_vdaf(b)
@@ -107,7 +112,7 @@ def _oracle_prep_share(b, agg_id, r, leader_in=None, public=None):
     return v.encode_prep_share(ps)
 
 
-@pytest.mark.parametrize("name", ["sum8", "hist4", "sumvec_small", "count"])
+@pytest.mark.parametrize("name", ["sum8", "hist4", "sumvec_small", "count", "fp16_3", "fp64_4"])
 def test_tampered_reports_rejected_alone(name):
     """A tampered leader measurement share fails decide for that report only; the GPU prep
     shares of the tampered report still match the oracle bit for bit."""
@@ -225,7 +230,7 @@ def test_rccl_merge_single_rank():
     comm.close()
 
 
-@pytest.mark.parametrize("name", list(SIZES))
+@pytest.mark.parametrize("name", [k for k in SIZES if k not in FPVEC])
 def test_gpu_shard_matches_oracle(name):
     """Client::shard + FLP prove on the GPU reproduce the oracle's public/leader/helper shares."""
     from tests.reports import meas_array
@@ -238,3 +243,65 @@ def test_gpu_shard_matches_oracle(name):
     if v.sizes.public_share:
         np.testing.assert_array_equal(pub, b.public)
     np.testing.assert_array_equal(lead, b.leader_in)
+
+
+def test_fixedpoint16_end_to_end_kat():
+    """interop_binaries/tests/end_to_end.rs:689-723 (e2e_prio3_fixed16vec): four FixedI16 vectors
+    of length 3 -> ["0.5", "0.5", "0.6875"], through the GPU leader + helper paths."""
+    from oracle import prio3 as O
+    from janus_amd.prio3 import Prio3Gpu
+    q = lambda x: int(x * (1 << 15))
+    ms = [[q(.25), q(.125), q(.125)], [q(.0625), q(.125), q(.0625)],
+          [q(.125), q(.125), q(.25)], [q(.0625), q(.125), q(.25)]]
+    ov = O.Prio3.new_fixedpoint_boundedl2_vec_sum(16, 3)
+    vk = bytes(range(16))
+    rows = {k: [] for k in ("nonce", "public_share", "leader_input_share", "helper_input_share")}
+    for i, m in enumerate(ms):
+        nonce = bytes([i + 1]) * 16
+        pub, shares = ov.shard(m, nonce, bytes([0x40 + i]) * ov.random_size())
+        rows["nonce"].append(nonce)
+        rows["public_share"].append(ov.encode_public_share(pub))
+        rows["leader_input_share"].append(ov.encode_input_share(shares[0]))
+        rows["helper_input_share"].append(ov.encode_input_share(shares[1]))
+    arr = {k: np.frombuffer(b"".join(v), np.uint8).reshape(len(v), -1).copy()
+           for k, v in rows.items()}
+    v = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(16, 3, vk)
+    ls, hs = v.new_state(0, 4), v.new_state(1, 4)
+    lp, lst = v.prepare_init(ls, arr["nonce"], arr["public_share"], arr["leader_input_share"])
+    hagg, lagg = v.new_aggregate(1), v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, arr["nonce"], arr["public_share"], arr["helper_input_share"], lp,
+                              agg=hagg)
+    assert (lst == 0).all() and (hst == 0).all()
+    v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
+    (la, lc), (ha, hc) = lagg.read(0), hagg.read(0)
+    assert lc == hc == 4
+    assert [repr(x) for x in v.unshard([la, ha], 4)] == ["0.5", "0.5", "0.6875"]
+
+
+def test_fixedpoint_norm_violation_rejected():
+    """A client that claims a smaller norm than its entries have (bit-encoded claim != computed
+    norm) is rejected by decide; the other reports of the batch are unaffected."""
+    from oracle import prio3 as O
+    b = batch("fp16_3")
+    v = gpu_vdaf(b)
+    ov = b.vdaf
+    typ = ov.typ
+    r = 2
+    # re-shard report r with a forged encoding: the norm bits claim 0
+    enc = typ.encode(b.measurements[r])
+    forged = enc[:typ.range_norm_begin] + [0] * typ.bits_for_norm
+    orig = typ.encode
+    typ.encode = lambda m: forged
+    try:
+        pub, shares = ov.shard(b.measurements[r], b.nonces[r].tobytes(), b.rand[r].tobytes())
+    finally:
+        typ.encode = orig
+    lin, hin, pb = b.leader_in.copy(), b.helper_in.copy(), b.public.copy()
+    lin[r] = np.frombuffer(ov.encode_input_share(shares[0]), np.uint8)
+    hin[r] = np.frombuffer(ov.encode_input_share(shares[1]), np.uint8)
+    pb[r] = np.frombuffer(ov.encode_public_share(pub), np.uint8)
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, pb, lin)
+    assert lp[r].tobytes() == _oracle_prep_share(b, 0, r, leader_in=lin, public=pb)
+    msgs, hst = v.helper_init(hs, b.nonces, pb, hin, lp, agg=v.new_aggregate(1))
+    assert hst[r] == 5 and (np.delete(hst, r) == 0).all()

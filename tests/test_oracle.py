@@ -74,7 +74,7 @@ def test_oracle_reproduces_golden(cfg):
         lo.append(v.fld.decode_vec(t["leader_out_share"]))
         ho.append(v.fld.decode_vec(t["helper_out_share"]))
     assert _enc(v.fld.encode_vec(v.aggregate(lo))) == cfg["leader_agg_share"]
-    assert v.unshard([v.aggregate(lo), v.aggregate(ho)]) == cfg["unsharded"]
+    assert v.unshard([v.aggregate(lo), v.aggregate(ho)], len(lo)) == cfg["unsharded"]
 
 
 @pytest.mark.parametrize("name", ["count", "sum8", "sum32", "sumvec_small", "countvec15", "hist4",
@@ -94,13 +94,53 @@ def test_c_restatement_matches_python(name):
     assert (res["status"] == 0).all() and res["count"] == 5
 
 
-@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_small", "hist4"])
+@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_small", "hist4", "fp16_3", "fp32_5"])
 def test_unshard_equals_plaintext(name):
     b = make_batch(name, 12)
     v = b.vdaf
     la = v.aggregate([v.fld.decode_vec(x.tobytes()) for x in b.leader_out])
     ha = v.aggregate([v.fld.decode_vec(x.tobytes()) for x in b.helper_out])
-    assert v.unshard([la, ha]) == plaintext_sum(b)
+    assert v.unshard([la, ha], b.n) == plaintext_sum(b)
+
+
+def _fp_run(bits, vecs):
+    v = O.Prio3.new_fixedpoint_boundedl2_vec_sum(bits, len(vecs[0]))
+    q = lambda x: int(x * (1 << (bits - 1)))
+    lo, ho = [], []
+    for i, m in enumerate(vecs):
+        t = O.run_vdaf(v, bytes(range(16)), bytes([i]) * 16, [q(x) for x in m],
+                       bytes([0x11 * (i + 1) & 0xFF]) * v.random_size())
+        lo.append(v.fld.decode_vec(t["leader_out_share"]))
+        ho.append(v.fld.decode_vec(t["helper_out_share"]))
+    return v.unshard([v.aggregate(lo), v.aggregate(ho)], len(vecs))
+
+
+def test_fixedpoint16_e2e_kat():
+    """interop_binaries/tests/end_to_end.rs:689-723: FixedI16 vectors -> ["0.5","0.5","0.6875"]."""
+    got = _fp_run(16, [[.25, .125, .125], [.0625, .125, .0625], [.125, .125, .25],
+                       [.0625, .125, .25]])
+    assert [repr(x) for x in got] == ["0.5", "0.5", "0.6875"]
+
+
+def test_fixedpoint32_collector_kat():
+    """collector/src/lib.rs:1033-1110: one FixedI32 report [1/16, 1/8, 1/4] -> same values;
+    end_to_end.rs e2e_prio3_fixed32vec uses the FP16 vectors at 32 bits -> same sums."""
+    assert _fp_run(32, [[.0625, .125, .25]]) == [0.0625, 0.125, 0.25]
+    got = _fp_run(32, [[.25, .125, .125], [.0625, .125, .0625], [.125, .125, .25],
+                       [.0625, .125, .25]])
+    assert got == [0.5, 0.5, 0.6875]
+
+
+def test_fixedpoint_shapes():
+    """Chunk lengths from prio's optimal_chunk_length; proof/verifier lengths of the two gadgets."""
+    v = O.Prio3.new_fixedpoint_boundedl2_vec_sum(16, 100000)
+    t = v.typ
+    assert t.MEAS_LEN == 16 * 100000 + 30
+    assert (t.chunk0, t.calls0, t.chunk1, t.calls1) == (1565, 1023, 393, 255)
+    assert v.PROOF_LEN == 2 * 1565 + 2 * 1023 + 1 + 393 + 2 * 255 + 1
+    assert v.VERIFIER_LEN == 1 + 2 * 1565 + 1 + 393 + 1
+    with pytest.raises(ValueError):  # norm >= 1 is not encodable
+        O.FixedPointBoundedL2VecSum(16, 2).encode([-(1 << 15), 0])
 
 
 def test_tampered_share_rejected_by_oracle():
