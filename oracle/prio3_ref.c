@@ -26,6 +26,7 @@
 typedef unsigned __int128 u128;
 typedef uint64_t u64;
 typedef uint8_t u8;
+typedef uint32_t u32;
 
 /* ============================ Keccak / SHAKE128 =========================================== */
 static const u64 RC[24] = {
@@ -301,17 +302,29 @@ static u128 poly_eval(const field* F, const u128* c, size_t n, u128 x) {
 }
 
 /* ============================ Prio3 types ================================================== */
-enum { K_COUNT = 0, K_SUM = 1, K_SUMVEC = 2, K_HIST = 3 };
+enum { K_COUNT = 0, K_SUM = 1, K_SUMVEC = 2, K_HIST = 3, K_FPVEC = 4 };
+/* gadget kinds (prio src/flp/gadgets.rs): Mul, PolyEval(x^2 - x), ParallelSum(Mul, chunk),
+ * ParallelSum(PolyEval(p), chunk) -- all of degree 2 */
+enum { G_MUL = 0, G_RANGE2 = 1, G_PSUM_MUL = 2, G_PSUM_POLY = 3 };
 
 typedef struct {
   int kind;
+  unsigned chunk, calls, arity, m, logm, gp_len;
+  u128 poly[3]; /* G_PSUM_POLY coefficients (Montgomery), ascending */
+} gadget;
+
+typedef struct {
+  int kind;
+  u32 algo_id;
   const field* F;
   unsigned bits, length, chunk;
-  unsigned meas_len, out_len, jr_len, prove_rand_len;
-  unsigned calls, arity, m, logm, gp_len, proof_len, ver_len;
+  unsigned meas_len, out_len, jr_len, qr_len, prove_rand_len;
+  unsigned ng;
+  gadget g[2];
+  unsigned proof_len, ver_len;
   u128 half; /* 1/2 Montgomery */
-  u128 roots[20]; /* roots[l] = principal 2^l-th root (Montgomery), prio FieldParameters.roots */
-  u128 ninv[20];  /* 1/2^l (Montgomery) */
+  u128 roots[24]; /* roots[l] = principal 2^l-th root (Montgomery), prio FieldParameters.roots */
+  u128 ninv[24];  /* 1/2^l (Montgomery) */
   u8 vk[16];
 } cfgt;
 
@@ -321,43 +334,93 @@ static unsigned npow2(unsigned x) {
   return r;
 }
 
+/* prio `optimal_chunk_length` (src/vdaf/prio3.rs): gadget_calls = 2^k - 1 from the largest k
+ * down, first minimum of the ParallelSum(Mul) proof length */
+static unsigned optimal_chunk_length(unsigned len) {
+  if (len <= 1) return 1;
+  unsigned max_log2 = 0;
+  { /* round(log2(len + 1)) */
+    double l = 0, x = (double)len + 1.0;
+    while (x >= 2.0) { x /= 2.0; l += 1.0; }
+    /* x in [1,2): log2(x) >= 0.5 iff x >= sqrt(2) */
+    max_log2 = (unsigned)l + (x >= 1.4142135623730951 ? 1 : 0);
+  }
+  unsigned long long best_cost = ~0ull;
+  unsigned best = 1;
+  for (unsigned k = max_log2; k >= 1; --k) {
+    unsigned long long calls = (1ull << k) - 1, chunk = (len + calls - 1) / calls;
+    unsigned long long cost = 2 * chunk + 2 * (npow2((unsigned)(1 + calls)) - 1) + 1;
+    if (cost < best_cost) { best_cost = cost; best = (unsigned)chunk; }
+  }
+  return best;
+}
+
+static void gadget_init(gadget* g, int kind, unsigned chunk, unsigned calls) {
+  g->kind = kind;
+  g->chunk = chunk;
+  g->calls = calls;
+  g->arity = kind == G_MUL ? 2 : kind == G_RANGE2 ? 1 : kind == G_PSUM_MUL ? 2 * chunk : chunk;
+  g->m = npow2(1 + calls);
+  g->logm = 0;
+  while ((1u << g->logm) < g->m) g->logm++;
+  g->gp_len = 2 * (g->m - 1) + 1;
+}
+
 int p3ref_cfg_init(cfgt* c, int kind, unsigned bits, unsigned length, unsigned chunk,
                    const u8 vk[16]) {
   memset(c, 0, sizeof *c);
   c->kind = kind;
+  c->algo_id = kind == K_FPVEC ? 0xFFFF0000u : (u32)kind;
   c->bits = bits;
   c->length = length;
   c->chunk = chunk;
+  c->qr_len = 1;
+  c->ng = 1;
   memcpy(c->vk, vk, 16);
   switch (kind) {
     case K_COUNT:
-      c->F = &F64; c->meas_len = 1; c->out_len = 1; c->jr_len = 0; c->calls = 1; c->arity = 2;
-      c->prove_rand_len = 2;
+      c->F = &F64; c->meas_len = 1; c->out_len = 1; c->jr_len = 0;
+      gadget_init(&c->g[0], G_MUL, 0, 1);
       break;
     case K_SUM:
-      c->F = &F128; c->meas_len = bits; c->out_len = 1; c->jr_len = 1; c->calls = bits;
-      c->arity = 1; c->prove_rand_len = 1;
+      c->F = &F128; c->meas_len = bits; c->out_len = 1; c->jr_len = 1;
+      gadget_init(&c->g[0], G_RANGE2, 0, bits);
       break;
     case K_SUMVEC:
       c->F = &F128; c->meas_len = bits * length; c->out_len = length; c->jr_len = 1;
-      c->calls = (c->meas_len + chunk - 1) / chunk; c->arity = 2 * chunk;
-      c->prove_rand_len = 2 * chunk;
+      gadget_init(&c->g[0], G_PSUM_MUL, chunk, (c->meas_len + chunk - 1) / chunk);
       break;
     case K_HIST:
       c->F = &F128; c->meas_len = length; c->out_len = length; c->jr_len = 2;
-      c->calls = (length + chunk - 1) / chunk; c->arity = 2 * chunk; c->prove_rand_len = 2 * chunk;
+      gadget_init(&c->g[0], G_PSUM_MUL, chunk, (length + chunk - 1) / chunk);
       break;
+    case K_FPVEC: {
+      if ((bits != 16 && bits != 32 && bits != 64) || length == 0) return -1;
+      c->F = &F128; c->meas_len = bits * length + 2 * bits - 2; c->out_len = length;
+      c->jr_len = 2; c->qr_len = 2; c->ng = 2;
+      unsigned c0 = optimal_chunk_length(c->meas_len), c1 = optimal_chunk_length(length);
+      gadget_init(&c->g[0], G_PSUM_MUL, c0, (c->meas_len + c0 - 1) / c0);
+      gadget_init(&c->g[1], G_PSUM_POLY, c1, (length + c1 - 1) / c1);
+      /* norm summand (z - 2^(n-1))^2 = 2^(2n-2) - 2^n z + z^2 */
+      const u128 one = (u128)1 << (bits - 1);
+      c->g[1].poly[0] = f_from_int(&F128, one * one);
+      c->g[1].poly[1] = f_sub(&F128, 0, f_from_int(&F128, 2 * one));
+      c->g[1].poly[2] = F128.one;
+      break;
+    }
     default:
       return -1;
   }
-  c->m = npow2(1 + c->calls);
-  c->logm = 0;
-  while ((1u << c->logm) < c->m) c->logm++;
-  c->gp_len = 2 * (c->m - 1) + 1;
-  c->proof_len = c->arity + c->gp_len;
-  c->ver_len = c->arity + 2;
+  c->proof_len = 0;
+  c->ver_len = 1;
+  c->prove_rand_len = 0;
+  for (unsigned i = 0; i < c->ng; ++i) {
+    c->proof_len += c->g[i].arity + c->g[i].gp_len;
+    c->ver_len += c->g[i].arity + 1;
+    c->prove_rand_len += c->g[i].arity;
+  }
   c->half = f_inv(c->F, f_from_int(c->F, 2));
-  for (unsigned l = 0; l < 20; ++l) {
+  for (unsigned l = 0; l < 24; ++l) {
     c->roots[l] = root_of_unity(c->F, l);
     c->ninv[l] = f_inv(c->F, f_from_int(c->F, (u128)1 << l));
   }
@@ -366,7 +429,8 @@ int p3ref_cfg_init(cfgt* c, int kind, unsigned bits, unsigned length, unsigned c
 
 static void dst(const cfgt* c, unsigned usage, u8 out[8]) {
   out[0] = 7; out[1] = 0;
-  out[2] = 0; out[3] = 0; out[4] = 0; out[5] = (u8)c->kind;
+  out[2] = (u8)(c->algo_id >> 24); out[3] = (u8)(c->algo_id >> 16);
+  out[4] = (u8)(c->algo_id >> 8); out[5] = (u8)c->algo_id;
   out[6] = (u8)(usage >> 8); out[7] = (u8)usage;
 }
 static void xof_init(const cfgt* c, shake* h, const u8 seed[16], unsigned usage) {
@@ -380,54 +444,51 @@ static void xof_init(const cfgt* c, shake* h, const u8 seed[16], unsigned usage)
 
 /* ---- gadget records ---------------------------------------------------------------------- */
 typedef struct {
+  const gadget* g;
   u128* f;      /* arity x (calls+1) wire values */
   unsigned ct;  /* next call index (1-based) */
   const u128* pvals; /* query: gadget poly evaluated at 2m-th roots (query mode) */
   int query;
 } shim;
 
-static u128 gadget_eval(const cfgt* c, const u128* inp) {
-  const field* F = c->F;
-  if (c->kind == K_SUM) { /* PolyEval x^2 - x */
-    return f_sub(F, f_mul(F, inp[0], inp[0]), inp[0]);
-  }
+static u128 gadget_eval(const field* F, const gadget* g, const u128* inp) {
   u128 acc = 0;
-  for (unsigned j = 0; j < c->arity / 2; ++j) acc = f_add(F, acc, f_mul(F, inp[2 * j], inp[2 * j + 1]));
-  return acc;
+  switch (g->kind) {
+    case G_MUL: return f_mul(F, inp[0], inp[1]);
+    case G_RANGE2: return f_sub(F, f_mul(F, inp[0], inp[0]), inp[0]);
+    case G_PSUM_MUL:
+      for (unsigned j = 0; j < g->chunk; ++j) acc = f_add(F, acc, f_mul(F, inp[2 * j], inp[2 * j + 1]));
+      return acc;
+    default: /* G_PSUM_POLY, Horner per input */
+      for (unsigned j = 0; j < g->chunk; ++j) {
+        u128 y = f_add(F, f_mul(F, g->poly[2], inp[j]), g->poly[1]);
+        acc = f_add(F, acc, f_add(F, f_mul(F, y, inp[j]), g->poly[0]));
+      }
+      return acc;
+  }
 }
 static u128 shim_call(const cfgt* c, shim* s, const u128* inp) {
-  for (unsigned w = 0; w < c->arity; ++w) s->f[w * (c->calls + 1) + s->ct] = inp[w];
-  u128 out = s->query ? s->pvals[s->ct * 2] : gadget_eval(c, inp);
+  const gadget* g = s->g;
+  for (unsigned w = 0; w < g->arity; ++w) s->f[w * (g->calls + 1) + s->ct] = inp[w];
+  u128 out = s->query ? s->pvals[s->ct * 2] : gadget_eval(c->F, g, inp);
   s->ct++;
   return out;
 }
 
-/* validity circuit with shim gadget (prio Type::valid) */
-static u128 valid(const cfgt* c, shim* g, const u128* x, const u128* jr, unsigned num_shares) {
+/* prio parallel_sum_range_checks: one joint-rand value, r_power across all chunks */
+static u128 psum_range_checks(const cfgt* c, shim* g, const u128* x, unsigned len, u128 r,
+                              u128 sinv) {
   const field* F = c->F;
-  if (c->kind == K_COUNT) {
-    u128 in[2] = {x[0], x[0]};
-    return f_sub(F, shim_call(c, g, in), x[0]);
-  }
-  if (c->kind == K_SUM) {
-    u128 r = jr[0], out = 0;
-    for (unsigned i = 0; i < c->bits; ++i) {
-      out = f_add(F, out, f_mul(F, r, shim_call(c, g, &x[i])));
-      r = f_mul(F, r, jr[0]);
-    }
-    return out;
-  }
-  /* parallel_sum_range_checks */
-  u128 sinv = num_shares == 2 ? c->half : F->one; /* 1/num_shares */
-  u128 out = 0, rp = jr[0];
-  u128* args = (u128*)malloc(sizeof(u128) * 2 * c->chunk);
-  for (unsigned k = 0; k < c->calls; ++k) {
-    for (unsigned j = 0; j < c->chunk; ++j) {
-      unsigned idx = k * c->chunk + j;
-      if (idx < c->meas_len) {
+  const unsigned chunk = g->g->chunk;
+  u128 out = 0, rp = r;
+  u128* args = (u128*)malloc(sizeof(u128) * 2 * chunk);
+  for (unsigned k = 0; k < g->g->calls; ++k) {
+    for (unsigned j = 0; j < chunk; ++j) {
+      unsigned idx = k * chunk + j;
+      if (idx < len) {
         args[2 * j] = f_mul(F, rp, x[idx]);
         args[2 * j + 1] = f_sub(F, x[idx], sinv);
-        rp = f_mul(F, rp, jr[0]);
+        rp = f_mul(F, rp, r);
       } else {
         args[2 * j] = 0;
         args[2 * j + 1] = f_sub(F, 0, sinv);
@@ -436,11 +497,55 @@ static u128 valid(const cfgt* c, shim* g, const u128* x, const u128* jr, unsigne
     out = f_add(F, out, shim_call(c, g, args));
   }
   free(args);
+  return out;
+}
+
+static u128 decode_bits(const field* F, const u128* x, unsigned nb) {
+  u128 acc = 0;
+  for (unsigned b = nb; b-- > 0;) acc = f_add(F, f_add(F, acc, acc), x[b]);
+  return acc;
+}
+
+/* validity circuit with shim gadgets (prio Type::valid) */
+static u128 valid(const cfgt* c, shim* g, const u128* x, const u128* jr, unsigned num_shares) {
+  const field* F = c->F;
+  if (c->kind == K_COUNT) {
+    u128 in[2] = {x[0], x[0]};
+    return f_sub(F, shim_call(c, &g[0], in), x[0]);
+  }
+  if (c->kind == K_SUM) {
+    u128 r = jr[0], out = 0;
+    for (unsigned i = 0; i < c->bits; ++i) {
+      out = f_add(F, out, f_mul(F, r, shim_call(c, &g[0], &x[i])));
+      r = f_mul(F, r, jr[0]);
+    }
+    return out;
+  }
+  u128 sinv = num_shares == 2 ? c->half : F->one; /* 1/num_shares */
+  u128 out = psum_range_checks(c, &g[0], x, c->meas_len, jr[0], sinv);
+  u128 r1 = jr[1];
   if (c->kind == K_HIST) {
     u128 sc = f_sub(F, 0, sinv);
     for (unsigned i = 0; i < c->meas_len; ++i) sc = f_add(F, sc, x[i]);
-    u128 r1 = jr[1];
     out = f_add(F, f_mul(F, r1, out), f_mul(F, f_mul(F, r1, r1), sc));
+  } else if (c->kind == K_FPVEC) {
+    /* prio FixedPointBoundedL2VecSum::valid: norm of the decoded entries by gadget 1, padded with
+     * the share of the encoded zero 2^(n-1)/num_shares; compared with the submitted norm bits */
+    const unsigned nb = c->bits, c1 = c->g[1].chunk;
+    const u128 zs = f_mul(F, f_from_int(F, (u128)1 << (nb - 1)), sinv);
+    u128* args = (u128*)malloc(sizeof(u128) * c1);
+    u128 computed = 0;
+    for (unsigned k = 0; k < c->g[1].calls; ++k) {
+      for (unsigned j = 0; j < c1; ++j) {
+        unsigned e = k * c1 + j;
+        args[j] = e < c->length ? decode_bits(F, &x[(size_t)e * nb], nb) : zs;
+      }
+      computed = f_add(F, computed, shim_call(c, &g[1], args));
+    }
+    free(args);
+    u128 submitted = decode_bits(F, &x[(size_t)nb * c->length], 2 * nb - 2);
+    u128 nc = f_sub(F, computed, submitted);
+    out = f_add(F, f_mul(F, r1, out), f_mul(F, f_mul(F, r1, r1), nc));
   }
   return out;
 }
@@ -449,80 +554,110 @@ static u128 valid(const cfgt* c, shim* g, const u128* x, const u128* jr, unsigne
 static void flp_prove(const cfgt* c, const u128* x, const u128* prove_rand, const u128* jr,
                       u128* proof) {
   const field* F = c->F;
-  const unsigned m = c->m, K = c->calls + 1;
-  shim s;
-  s.f = (u128*)calloc((size_t)c->arity * K, sizeof(u128));
-  s.ct = 1;
-  s.query = 0;
-  for (unsigned w = 0; w < c->arity; ++w) s.f[w * K] = prove_rand[w];
-  (void)valid(c, &s, x, jr, 1);
-  /* wire polys: interpolate, then evaluate at 2m points */
-  const unsigned n2 = 2 * m;
-  u128* coef = (u128*)malloc(sizeof(u128) * m);
-  u128* ev = (u128*)malloc(sizeof(u128) * n2 * c->arity);
-  for (unsigned w = 0; w < c->arity; ++w) {
-    dft(F, c->roots, coef, &s.f[w * K], K, m);
-    idft_finish(F, c->ninv[c->logm], coef, m);
-    proof[w] = s.f[w * K];
-    dft(F, c->roots, &ev[(size_t)w * n2], coef, m, n2);
+  shim s[2];
+  unsigned pr = 0;
+  for (unsigned i = 0; i < c->ng; ++i) {
+    const gadget* g = &c->g[i];
+    const unsigned K = g->calls + 1;
+    s[i].g = g;
+    s[i].f = (u128*)calloc((size_t)g->arity * K, sizeof(u128));
+    s[i].ct = 1;
+    s[i].query = 0;
+    for (unsigned w = 0; w < g->arity; ++w) s[i].f[w * K] = prove_rand[pr++];
   }
-  /* gadget poly values at 2m points, then interpolate */
-  u128* gv = (u128*)malloc(sizeof(u128) * n2);
-  for (unsigned i = 0; i < n2; ++i) {
-    u128 in[512];
-    u128* inp = c->arity <= 512 ? in : (u128*)malloc(sizeof(u128) * c->arity);
-    for (unsigned w = 0; w < c->arity; ++w) inp[w] = ev[(size_t)w * n2 + i];
-    gv[i] = gadget_eval(c, inp);
-    if (inp != in) free(inp);
+  (void)valid(c, s, x, jr, 1);
+  size_t off = 0;
+  for (unsigned i = 0; i < c->ng; ++i) {
+    const gadget* g = &c->g[i];
+    const unsigned m = g->m, K = g->calls + 1;
+    /* wire polys: interpolate, then evaluate at 2m points */
+    const unsigned n2 = 2 * m;
+    u128* coef = (u128*)malloc(sizeof(u128) * m);
+    u128* ev = (u128*)malloc(sizeof(u128) * n2 * g->arity);
+    for (unsigned w = 0; w < g->arity; ++w) {
+      dft(F, c->roots, coef, &s[i].f[w * K], K, m);
+      idft_finish(F, c->ninv[g->logm], coef, m);
+      proof[off + w] = s[i].f[w * K];
+      dft(F, c->roots, &ev[(size_t)w * n2], coef, m, n2);
+    }
+    /* gadget poly values at 2m points, then interpolate */
+    u128* gv = (u128*)malloc(sizeof(u128) * n2);
+    u128* inp = (u128*)malloc(sizeof(u128) * g->arity);
+    for (unsigned q = 0; q < n2; ++q) {
+      for (unsigned w = 0; w < g->arity; ++w) inp[w] = ev[(size_t)w * n2 + q];
+      gv[q] = gadget_eval(F, g, inp);
+    }
+    u128* gp = (u128*)malloc(sizeof(u128) * n2);
+    dft(F, c->roots, gp, gv, n2, n2);
+    idft_finish(F, c->ninv[g->logm + 1], gp, n2);
+    for (unsigned d = 0; d < g->gp_len; ++d) proof[off + g->arity + d] = gp[d];
+    off += g->arity + g->gp_len;
+    free(gp); free(inp); free(gv); free(ev); free(coef); free(s[i].f);
   }
-  u128* gp = (u128*)malloc(sizeof(u128) * n2);
-  dft(F, c->roots, gp, gv, n2, n2);
-  idft_finish(F, c->ninv[c->logm + 1], gp, n2);
-  for (unsigned d = 0; d < c->gp_len; ++d) proof[c->arity + d] = gp[d];
-  free(gp); free(gv); free(ev); free(coef); free(s.f);
 }
 
 /* FLP query (prio flp.rs Type::query): returns 0 on invalid query randomness */
-static int flp_query(const cfgt* c, const u128* x, const u128* proof, u128 t, const u128* jr,
-                     u128* verifier) {
+static int flp_query(const cfgt* c, const u128* x, const u128* proof, const u128* t,
+                     const u128* jr, u128* verifier) {
   const field* F = c->F;
-  const unsigned m = c->m, K = c->calls + 1;
-  if (f_pow(F, t, m) == F->one) return 0;
-  shim s;
-  s.f = (u128*)calloc((size_t)c->arity * K, sizeof(u128));
-  s.ct = 1;
-  s.query = 1;
-  for (unsigned w = 0; w < c->arity; ++w) s.f[w * K] = proof[w];
-  u128* pv = (u128*)malloc(sizeof(u128) * 2 * m);
-  dft(F, c->roots, pv, &proof[c->arity], c->gp_len, 2 * m);
-  s.pvals = pv;
-  verifier[0] = valid(c, &s, x, jr, 2);
-  u128* coef = (u128*)malloc(sizeof(u128) * m);
-  for (unsigned w = 0; w < c->arity; ++w) {
-    dft(F, c->roots, coef, &s.f[w * K], K, m);
-    idft_finish(F, c->ninv[c->logm], coef, m);
-    verifier[1 + w] = poly_eval(F, coef, m, t);
+  shim s[2];
+  u128* pv[2] = {NULL, NULL};
+  size_t off = 0;
+  int ok = 1;
+  for (unsigned i = 0; i < c->ng; ++i) {
+    const gadget* g = &c->g[i];
+    const unsigned K = g->calls + 1;
+    if (f_pow(F, t[i], g->m) == F->one) ok = 0;
+    s[i].g = g;
+    s[i].f = (u128*)calloc((size_t)g->arity * K, sizeof(u128));
+    s[i].ct = 1;
+    s[i].query = 1;
+    for (unsigned w = 0; w < g->arity; ++w) s[i].f[w * K] = proof[off + w];
+    pv[i] = (u128*)malloc(sizeof(u128) * 2 * g->m);
+    dft(F, c->roots, pv[i], &proof[off + g->arity], g->gp_len, 2 * g->m);
+    s[i].pvals = pv[i];
+    off += g->arity + g->gp_len;
   }
-  verifier[1 + c->arity] = poly_eval(F, &proof[c->arity], c->gp_len, t);
-  free(coef); free(pv); free(s.f);
+  if (!ok) {
+    for (unsigned i = 0; i < c->ng; ++i) { free(s[i].f); free(pv[i]); }
+    return 0;
+  }
+  verifier[0] = valid(c, s, x, jr, 2);
+  size_t vo = 1;
+  off = 0;
+  for (unsigned i = 0; i < c->ng; ++i) {
+    const gadget* g = &c->g[i];
+    const unsigned m = g->m, K = g->calls + 1;
+    u128* coef = (u128*)malloc(sizeof(u128) * m);
+    for (unsigned w = 0; w < g->arity; ++w) {
+      dft(F, c->roots, coef, &s[i].f[w * K], K, m);
+      idft_finish(F, c->ninv[g->logm], coef, m);
+      verifier[vo++] = poly_eval(F, coef, m, t[i]);
+    }
+    verifier[vo++] = poly_eval(F, &proof[off + g->arity], g->gp_len, t[i]);
+    off += g->arity + g->gp_len;
+    free(coef); free(pv[i]); free(s[i].f);
+  }
   return 1;
 }
 
 static int flp_decide(const cfgt* c, const u128* v) {
   if (v[0] != 0) return 0;
-  return gadget_eval(c, &v[1]) == v[1 + c->arity];
+  size_t vo = 1;
+  for (unsigned i = 0; i < c->ng; ++i) {
+    const gadget* g = &c->g[i];
+    if (gadget_eval(c->F, g, &v[vo]) != v[vo + g->arity]) return 0;
+    vo += g->arity + 1;
+  }
+  return 1;
 }
 
 /* truncate (prio Type::truncate), Montgomery in/out */
 static void truncate_out(const cfgt* c, const u128* x, u128* out) {
   const field* F = c->F;
-  if (c->kind == K_SUM || c->kind == K_SUMVEC) {
+  if (c->kind == K_SUM || c->kind == K_SUMVEC || c->kind == K_FPVEC) {
     unsigned len = c->kind == K_SUM ? 1 : c->length;
-    for (unsigned e = 0; e < len; ++e) {
-      u128 acc = 0;
-      for (unsigned b = c->bits; b-- > 0;) acc = f_add(F, f_add(F, acc, acc), x[e * c->bits + b]);
-      out[e] = acc;
-    }
+    for (unsigned e = 0; e < len; ++e) out[e] = decode_bits(F, &x[(size_t)e * c->bits], c->bits);
   } else {
     memcpy(out, x, sizeof(u128) * c->out_len);
   }
@@ -615,13 +750,13 @@ static void shard(const cfgt* c, const u128* encoded, const u8 nonce[16], const 
 static int prepare_init(const cfgt* c, int agg_id, const u8 nonce[16], const u8* pub,
                         const u8* share, u8* prep_share, u128* out_share, u8 seed[16]) {
   const field* F = c->F;
-  u128 t;
+  u128 t[2];
   {
     shake h;
     xof_init(c, &h, c->vk, 5);
     shake_absorb(&h, nonce, 16);
     shake_finish(&h);
-    xof_next_vec(F, &h, &t, 1);
+    xof_next_vec(F, &h, t, c->qr_len);
   }
   u128* meas = (u128*)malloc(sizeof(u128) * c->meas_len);
   u128* proof = (u128*)malloc(sizeof(u128) * c->proof_len);
@@ -716,6 +851,37 @@ static void synth(const cfgt* c, const u8* cfg_id, size_t cfg_len, u64 i, u8 non
   shake_squeeze(&h, rand, rs);
   const field* F = c->F;
   for (unsigned k = 0; k < c->meas_len; ++k) encoded[k] = 0;
+  if (c->kind == K_FPVEC) {
+    /* integer entries uniform in [-B, B], entries * B^2 <= (2^(n-1)-1)^2
+     * (oracle/prio3.py synth_fixedpoint), 8 stream bytes per entry */
+    const unsigned nb = c->bits;
+    const u128 one = ((u128)1 << (nb - 1)) - 1;
+    const u128 q = one * one / c->length;
+    u128 B = 0;
+    { /* isqrt */
+      u128 lo = 0, hi = (u128)1 << 64;
+      while (lo < hi) {
+        u128 mid = (lo + hi + 1) / 2;
+        if (mid * mid <= q) lo = mid; else hi = mid - 1;
+      }
+      B = lo;
+    }
+    u128 norm = 0;
+    for (unsigned e = 0; e < c->length; ++e) {
+      u8 b[8];
+      shake_squeeze(&h, b, 8);
+      u64 v = 0;
+      for (int k = 0; k < 8; ++k) v |= (u64)b[k] << (8 * k);
+      long long sv = (long long)((u128)v % (2 * B + 1)) - (long long)B;
+      meas_out[e] = (u64)sv;
+      const u64 z = (u64)sv + ((u64)1 << (nb - 1)); /* two's complement with the top bit flipped */
+      for (unsigned k = 0; k < nb; ++k) encoded[(size_t)e * nb + k] = (z >> k & 1) ? F->one : 0;
+      norm += (u128)((__int128)sv * sv);
+    }
+    for (unsigned k = 0; k < 2 * nb - 2; ++k)
+      encoded[(size_t)nb * c->length + k] = (norm >> k & 1) ? F->one : 0;
+    return;
+  }
   if (c->kind == K_SUMVEC) {
     unsigned nb = (c->bits + 7) / 8;
     for (unsigned e = 0; e < c->length; ++e) {
@@ -767,7 +933,7 @@ static void* gen_worker(void* arg) {
   const cfgt* c = &j->r->c;
   const unsigned rs = p3ref_random_size(c);
   const unsigned L = p3ref_leader_len(c), H = p3ref_helper_len(c), P = p3ref_public_len(c);
-  const unsigned mw = c->kind == K_SUMVEC ? c->length : 1;
+  const unsigned mw = (c->kind == K_SUMVEC || c->kind == K_FPVEC) ? c->length : 1;
   u8* rand = (u8*)malloc(rs);
   u128* enc = (u128*)malloc(sizeof(u128) * c->meas_len);
   for (size_t k = j->lo; k < j->hi; ++k) {
@@ -904,7 +1070,7 @@ static void* synth_worker(void* arg) {
   synth_job* j = (synth_job*)arg;
   const cfgt* c = &j->r->c;
   const unsigned rs = p3ref_random_size(c);
-  const unsigned mw = c->kind == K_SUMVEC ? c->length : 1;
+  const unsigned mw = (c->kind == K_SUMVEC || c->kind == K_FPVEC) ? c->length : 1;
   u128* enc = (u128*)malloc(sizeof(u128) * c->meas_len);
   for (size_t k = j->lo; k < j->hi; ++k)
     synth(c, j->cfg_id, j->cfg_len, j->start + k, j->nonces + 16 * k, j->rand + (size_t)rs * k, enc,

@@ -71,7 +71,7 @@ class Prio3Ref:
             public=np.zeros((n, self.public_len), np.uint8),
             leader_in=np.zeros((n, self.leader_len), np.uint8),
             helper_in=np.zeros((n, self.helper_len), np.uint8),
-            meas=np.zeros((n, self.length if self.kind == 2 else 1), np.uint64),
+            meas=np.zeros((n, self.length if self.kind in (2, 4) else 1), np.uint64),
         )
         lib().p3ref_gen(self._h, _p(cid), len(cfg_id), start, n, threads, _p(out["nonces"]),
                         _p(out["public"]) if self.public_len else None, _p(out["leader_in"]),
@@ -84,7 +84,7 @@ class Prio3Ref:
         cid = np.frombuffer(cfg_id, dtype=np.uint8).copy()
         out = dict(nonces=np.zeros((n, 16), np.uint8),
                    rand=np.zeros((n, self.random_size), np.uint8),
-                   meas=np.zeros((n, self.length if self.kind == 2 else 1), np.uint64))
+                   meas=np.zeros((n, self.length if self.kind in (2, 4) else 1), np.uint64))
         lib().p3ref_synth(self._h, _p(cid), len(cfg_id), start, n, threads, _p(out["nonces"]),
                           _p(out["rand"]), _p(out["meas"]))
         return out

@@ -305,3 +305,33 @@ def test_fixedpoint_norm_violation_rejected():
     assert lp[r].tobytes() == _oracle_prep_share(b, 0, r, leader_in=lin, public=pb)
     msgs, hst = v.helper_init(hs, b.nonces, pb, hin, lp, agg=v.new_aggregate(1))
     assert hst[r] == 5 and (np.delete(hst, r) == 0).all()
+
+
+def test_fixedpoint16_100k_entries_config_e():
+    """BASELINE config E (FixedI16 BoundedL2VecSum, 100k entries: 1.6M-element shares, 25.7 MB
+    per leader share): GPU prep shares, prep msgs and both aggregate shares bit-exact against the
+    C restatement; unshard == the plaintext sum."""
+    from oracle import prio3 as O
+    from oracle.ref import Prio3Ref
+    from janus_amd.prio3 import Prio3Gpu
+    vk = O.synth_verify_key(b"cfgE")
+    ref = Prio3Ref(4, vk, 16, 100000, 0)
+    n = 3
+    g = ref.gen(b"cfgE", 0, n, threads=16)
+    res = ref.prepare_batch(g["nonces"], g["public"], g["leader_in"], g["helper_in"], threads=16)
+    assert (res["status"] == 0).all()
+    v = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(16, 100000, vk)
+    ls, hs = v.new_state(0, n), v.new_state(1, n)
+    lp, lst = v.prepare_init(ls, g["nonces"], g["public"], g["leader_in"])
+    assert (lst == 0).all()
+    np.testing.assert_array_equal(lp, res["lprep"])
+    hagg, lagg = v.new_aggregate(1), v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, g["nonces"], g["public"], g["helper_in"], lp, agg=hagg)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(msgs, res["msgs"])
+    v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
+    (la, lc), (ha, hc) = lagg.read(0), hagg.read(0)
+    assert lc == hc == n
+    assert la == res["agg_l"].tobytes() and ha == res["agg_h"].tobytes()
+    plain = g["meas"].view(np.int64).sum(axis=0) * 2.0 ** -15
+    assert v.unshard([la, ha], n) == pytest.approx(list(plain), abs=1e-12)

@@ -78,7 +78,7 @@ def test_oracle_reproduces_golden(cfg):
 
 
 @pytest.mark.parametrize("name", ["count", "sum8", "sum32", "sumvec_small", "countvec15", "hist4",
-                                  "hist256"])
+                                  "hist256", "fp16_3", "fp32_5", "fp64_4", "fp16_300"])
 def test_c_restatement_matches_python(name):
     from oracle.ref import Prio3Ref
     b = make_batch(name, 5)
@@ -87,6 +87,8 @@ def test_c_restatement_matches_python(name):
     g = r.gen(name.encode(), 0, 5, threads=2)
     for k in ["nonces", "public", "leader_in", "helper_in"]:
         np.testing.assert_array_equal(g[k], getattr(b, k))
+    if c["kind"] == 4:  # fixed-point measurements are signed (two's complement in the u64 words)
+        np.testing.assert_array_equal(g["meas"].view(np.int64), np.array(b.measurements))
     res = r.prepare_batch(b.nonces, b.public, b.leader_in, b.helper_in, threads=2)
     np.testing.assert_array_equal(res["lprep"], b.leader_prep)
     np.testing.assert_array_equal(res["hprep"], b.helper_prep)
