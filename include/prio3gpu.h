@@ -198,6 +198,88 @@ int prio3gpu_dev_alloc(prio3gpu_ctx* ctx, size_t bytes, void** out);
 int prio3gpu_dev_free(prio3gpu_ctx* ctx, void* p);
 int prio3gpu_memcpy(prio3gpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 
+/* ---- DAP codec edge (host-only; janus_amd/csrc/codec.cpp) ------------------------------------
+ * Batched decode/encode of the aggregate-init messages around the engine,
+ * replacing the per-report Decode/Encode calls of the helper and leader loops:
+ *   helper  AggregationJobInitializeReq::get_decoded   aggregator.rs:1561-1612 (request body)
+ *           PlaintextInputShare::get_decoded + InputShare/PublicShare::get_decoded_with_param
+ *                                                        aggregator.rs:1702-1768
+ *           AggregationJobResp::get_encoded             aggregator.rs:1811-1848
+ *   leader  AggregationJobInitializeReq::new + encode   aggregation_job_driver.rs:329-437
+ *           AggregationJobResp::get_decoded             aggregation_job_driver.rs:530-600
+ * Message layouts: messages/src/lib.rs (see codec.cpp).  Offsets are byte offsets into `msg`.
+ * query_type: 1 = TimeInterval, 2 = FixedSize (lib.rs:2024-2028). */
+typedef struct prio3gpu_prepare_init_view {
+  uint64_t report_id_off;    /* 16-byte ReportId (= VDAF nonce) */
+  uint64_t time;             /* ReportMetadata time, seconds since the epoch */
+  uint64_t public_share_off;
+  uint64_t enc_off;          /* HpkeCiphertext encapsulated key */
+  uint64_t payload_off;      /* HpkeCiphertext payload */
+  uint64_t prep_share_off;   /* PingPongMessage Initialize/Continue prep share */
+  uint64_t prep_msg_off;     /* PingPongMessage Continue/Finish prep msg */
+  uint32_t public_share_len, enc_len, payload_len, prep_share_len, prep_msg_len;
+  uint8_t hpke_config_id;
+  uint8_t message_type;      /* 0 Initialize, 1 Continue, 2 Finish */
+} prio3gpu_prepare_init_view;
+
+typedef struct prio3gpu_prepare_resp_view {
+  uint64_t report_id_off;
+  uint64_t prep_share_off, prep_msg_off;
+  uint32_t prep_share_len, prep_msg_len;
+  uint8_t result;            /* PrepareStepResult: 0 Continue, 1 Finished, 2 Reject */
+  uint8_t message_type;      /* Continue: PingPongMessage type */
+  uint8_t error;             /* Reject: PrepareError */
+} prio3gpu_prepare_resp_view;
+
+/* AggregationJobInitializeReq -> one view per PrepareInit.  views == NULL counts only.
+ * out_agg_param (may be NULL) = {offset, length}; out_batch_id (FixedSize, may be NULL) 32 bytes.
+ * A malformed request is an API error (Janus rejects the whole request). */
+int prio3gpu_decode_agg_init_req(const uint8_t* msg, size_t len, int query_type,
+                                 uint8_t* out_batch_id, uint64_t* out_agg_param,
+                                 prio3gpu_prepare_init_view* views, size_t max_views,
+                                 size_t* out_n);
+/* Helper: pack the engine inputs of n PrepareInits (nonces n x 16, public shares, leader prep
+ * shares).  Public share of the wrong length -> InvalidMessage; a message that is not
+ * Initialize{prep share of the right length} -> VdafPrepError.  status in/out. */
+int prio3gpu_gather_prepare_inits(const prio3gpu_sizes* sizes, const uint8_t* msg,
+                                  const prio3gpu_prepare_init_view* views, size_t n,
+                                  uint8_t* nonces, uint8_t* public_shares,
+                                  uint8_t* leader_prep_shares, uint8_t* status);
+/* HPKE-opened PlaintextInputShares (report i = plaintexts[offsets[i] .. offsets[i+1])) ->
+ * n x input share (agg_id 0: leader, 1: helper).  Undecodable, duplicate extensions or wrong
+ * payload length -> InvalidMessage.  status in/out. */
+int prio3gpu_decode_plaintext_input_shares(const prio3gpu_sizes* sizes, const uint8_t* plaintexts,
+                                           const uint64_t* offsets, size_t n, int agg_id,
+                                           uint8_t* out_input_shares, uint8_t* status);
+/* Helper: AggregationJobResp from the batch outputs: status 0 -> Continue{Finish{prep msg}},
+ * otherwise Reject(status).  out == NULL (or too small) reports the length in out_len. */
+int prio3gpu_encode_agg_job_resp(const uint8_t* nonces, const uint8_t* prep_msgs,
+                                 uint32_t prep_msg_len, const uint8_t* status, size_t n,
+                                 uint8_t* out, size_t cap, size_t* out_len);
+/* Leader: AggregationJobInitializeReq for the reports whose status is 0 (status may be NULL):
+ * ReportShare{id, time, public share, HpkeCiphertext{config id, enc, payload}} +
+ * Initialize{leader prep share}.  Variable-length enc/payload use offset arrays (n + 1). */
+int prio3gpu_encode_agg_init_req(int query_type, const uint8_t* batch_id, const uint8_t* agg_param,
+                                 uint32_t agg_param_len, size_t n, const uint8_t* nonces,
+                                 const uint64_t* times, const uint8_t* public_shares,
+                                 uint32_t public_share_len, const uint8_t* hpke_config_ids,
+                                 const uint8_t* encs, const uint64_t* enc_offsets,
+                                 const uint8_t* payloads, const uint64_t* payload_offsets,
+                                 const uint8_t* prep_shares, uint32_t prep_share_len,
+                                 const uint8_t* status, uint8_t* out, size_t cap,
+                                 size_t* out_len);
+/* AggregationJobResp -> one view per PrepareResp (views == NULL counts only). */
+int prio3gpu_decode_agg_job_resp(const uint8_t* msg, size_t len,
+                                 prio3gpu_prepare_resp_view* views, size_t max_views,
+                                 size_t* out_n);
+/* Leader: match the helper's responses to the n reports it sent (status 0 ones, in order):
+ * Continue{Finish{prep msg}} -> prep msg; Reject(e) -> status e; anything else -> VdafPrepError.
+ * A response for an unexpected report ID is an API error (the job fails). */
+int prio3gpu_gather_helper_resps(const prio3gpu_sizes* sizes, const uint8_t* msg,
+                                 const prio3gpu_prepare_resp_view* views, size_t n_views,
+                                 const uint8_t* nonces, size_t n, uint8_t* prep_msgs,
+                                 uint8_t* status);
+
 /* Last error message for this thread (static storage). */
 const char* prio3gpu_last_error(void);
 

@@ -28,7 +28,7 @@ class Prio3GpuError(RuntimeError):
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP engine for gfx950 into janus_amd/lib/libprio3gpu.so."""
-    srcs = [CSRC / "engine.hip"]
+    srcs = [CSRC / "engine.hip", CSRC / "codec.cpp"]
     deps = srcs + list(CSRC.glob("*.h")) + [INCLUDE / "prio3gpu.h"]
     if LIB_PATH.exists() and not force:
         newest = max(p.stat().st_mtime for p in deps)
@@ -37,7 +37,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     LIB_DIR.mkdir(exist_ok=True)
     tmp = LIB_PATH.with_suffix(".so.tmp")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", str(tmp), str(srcs[0]), "-lrccl"]
+           "-o", str(tmp)] + [str(x) for x in srcs] + ["-lrccl"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -80,6 +80,22 @@ def _declare(lib):
         "prio3gpu_dev_free": (c.c_int, [P, P]),
         "prio3gpu_memcpy": (c.c_int, [P, P, P, c.c_size_t]),
         "prio3gpu_last_error": (c.c_char_p, []),
+        # DAP codec edge (host-only, codec.cpp)
+        "prio3gpu_decode_agg_init_req": (c.c_int, [u8p, c.c_size_t, c.c_int, u8p, P, P, c.c_size_t,
+                                                   c.POINTER(c.c_size_t)]),
+        "prio3gpu_gather_prepare_inits": (c.c_int, [P, u8p, P, c.c_size_t, u8p, u8p, u8p, u8p]),
+        "prio3gpu_decode_plaintext_input_shares": (c.c_int, [P, u8p, P, c.c_size_t, c.c_int, u8p,
+                                                             u8p]),
+        "prio3gpu_encode_agg_job_resp": (c.c_int, [u8p, u8p, c.c_uint32, u8p, c.c_size_t, u8p,
+                                                   c.c_size_t, c.POINTER(c.c_size_t)]),
+        "prio3gpu_encode_agg_init_req": (c.c_int, [c.c_int, u8p, u8p, c.c_uint32, c.c_size_t, u8p,
+                                                   P, u8p, c.c_uint32, u8p, u8p, P, u8p, P, u8p,
+                                                   c.c_uint32, u8p, u8p, c.c_size_t,
+                                                   c.POINTER(c.c_size_t)]),
+        "prio3gpu_decode_agg_job_resp": (c.c_int, [u8p, c.c_size_t, P, c.c_size_t,
+                                                   c.POINTER(c.c_size_t)]),
+        "prio3gpu_gather_helper_resps": (c.c_int, [P, u8p, P, c.c_size_t, u8p, c.c_size_t, u8p,
+                                                   u8p]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -98,7 +114,9 @@ EXPORTED = [
     "prio3gpu_random_size", "prio3gpu_shard", "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
     "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
     "prio3gpu_prof_kernel_name", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
-    "prio3gpu_last_error",
+    "prio3gpu_last_error", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
+    "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",
+    "prio3gpu_encode_agg_init_req", "prio3gpu_decode_agg_job_resp", "prio3gpu_gather_helper_resps",
 ]
 
 

@@ -1,0 +1,180 @@
+"""DAP codec edge (janus_amd/codec.py -> native codec.cpp in libprio3gpu.so) against the
+reference's own message KATs (messages/src/lib.rs:3346-3400, :4282-4557, :4616-4665, stored as
+data in tests/golden/dap_framing_kats.json), the per-report error mapping of the helper loop
+(aggregator/src/aggregator.rs:1702-1797), and a full leader <-> helper message round trip through
+the GPU engine (gpu-marked)."""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from janus_amd import codec as C
+from janus_amd import messages as M
+from janus_amd.prio3 import _Sizes
+
+KATS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "dap_framing_kats.json")))
+h = lambda s: bytes.fromhex(s.replace(" ", ""))
+
+
+def _sizes(public_share=0, prep_share=6, prep_msg=0, helper_input_share=4):
+    s = _Sizes()
+    s.public_share, s.prep_share, s.prep_msg = public_share, prep_share, prep_msg
+    s.helper_input_share, s.leader_input_share = helper_input_share, helper_input_share
+    return s
+
+
+@pytest.mark.parametrize("qt,key", [(C.TIME_INTERVAL, "time_interval"), (C.FIXED_SIZE, "fixed_size")])
+def test_decode_agg_init_req_kat(qt, key):
+    k = KATS["agg_init_req"]
+    req = C.decode_agg_init_req(h(k[key]), qt)
+    assert req.n == 2 and req.agg_param == h(k["agg_param"])
+    if qt == C.FIXED_SIZE:
+        assert req.batch_id == b"\x02" * 32
+    for i, rep in enumerate(k["reports"]):
+        v = req.views[i]
+        assert req.raw[v.report_id_off:v.report_id_off + 16].tobytes() == h(rep["report_id"])
+        assert v.time == rep["time"] and v.hpke_config_id == rep["config_id"]
+        assert req.field(i, "public_share_off", "public_share_len") == h(rep["public_share"])
+        assert req.hpke_ciphertexts()[i] == (rep["config_id"], h(rep["enc"]), h(rep["payload"]))
+        assert v.message_type == rep["message"]["type"]
+        if v.message_type == 0:
+            assert req.field(i, "prep_share_off", "prep_share_len") == h(rep["message"]["prep_share"])
+    # wrong query type / truncated / trailing bytes: the whole request is rejected
+    with pytest.raises(Exception):
+        C.decode_agg_init_req(h(k[key]), C.FIXED_SIZE if qt == C.TIME_INTERVAL else C.TIME_INTERVAL)
+    with pytest.raises(Exception):
+        C.decode_agg_init_req(h(k[key])[:-1], qt)
+    with pytest.raises(Exception):
+        C.decode_agg_init_req(h(k[key]) + b"\x00", qt)
+
+
+def test_gather_prepare_inits_error_mapping():
+    """Report 0 (Initialize, 6-byte prep share, empty public share) is accepted; report 1 has a
+    4-byte public share (InvalidMessage when the VDAF expects none) and carries Finish instead of
+    Initialize (VdafPrepError once its public share decodes)."""
+    k = KATS["agg_init_req"]
+    req = C.decode_agg_init_req(h(k["time_interval"]))
+    nonces, pub, lps, st = C.gather_prepare_inits(_sizes(), req)
+    assert list(st) == [0, 8]
+    assert nonces[0].tobytes() == h(k["reports"][0]["report_id"])
+    assert lps[0].tobytes() == h("303132333435")
+    _, _, _, st = C.gather_prepare_inits(_sizes(public_share=4), req)
+    assert list(st) == [8, 5]
+
+
+def test_encode_agg_init_req_matches_kat_bytes():
+    k = KATS["agg_init_req"]
+    rep = k["reports"][0]
+    got = C.encode_agg_init_req(
+        C.TIME_INTERVAL, None, h(k["agg_param"]), np.frombuffer(h(rep["report_id"]), np.uint8)[None],
+        [rep["time"]], np.zeros((1, 0), np.uint8), [(rep["config_id"], h(rep["enc"]), h(rep["payload"]))],
+        np.frombuffer(h(rep["message"]["prep_share"]), np.uint8)[None])
+    full = h(k["time_interval"])
+    pi1 = full[4 + 6 + 1 + 4:4 + 6 + 1 + 4 + 58]  # first PrepareInit of the KAT encoding
+    assert got == full[:11] + struct.pack(">I", len(pi1)) + pi1
+    # the FixedSize header, and a report with failed leader prepare_init is not sent
+    got = C.encode_agg_init_req(
+        C.FIXED_SIZE, b"\x02" * 32, h(k["agg_param"]),
+        np.frombuffer(h(rep["report_id"]) * 2, np.uint8).reshape(2, 16), [rep["time"]] * 2,
+        np.zeros((2, 0), np.uint8), [(rep["config_id"], h(rep["enc"]), h(rep["payload"]))] * 2,
+        np.frombuffer(h(rep["message"]["prep_share"]) * 2, np.uint8).reshape(2, 6),
+        status=np.array([0, 5], np.uint8))
+    fs = h(k["fixed_size"])
+    assert got == fs[:11 + 32] + struct.pack(">I", len(pi1)) + pi1
+
+
+def test_decode_agg_job_resp_kat():
+    raw, views, n = C.decode_agg_job_resp(h(KATS["agg_job_resp"]["expected"]))
+    assert n == 2
+    assert views[0].result == 0 and views[0].message_type == 1
+    o, l = views[0].prep_msg_off, views[0].prep_msg_len
+    assert raw[o:o + l].tobytes() == b"01234"
+    o, l = views[0].prep_share_off, views[0].prep_share_len
+    assert raw[o:o + l].tobytes() == b"56789"
+    assert views[1].result == 1
+    # neither is Continue{Finish{prep msg}}: both reports fail (ping-pong mismatch)
+    nonces = np.frombuffer(bytes(range(1, 17)) + bytes(range(16, 0, -1)), np.uint8).reshape(2, 16)
+    _, st = C.gather_helper_resps(_sizes(prep_msg=5), h(KATS["agg_job_resp"]["expected"]), nonces,
+                                  np.zeros(2, np.uint8))
+    assert list(st) == [5, 5]
+    with pytest.raises(Exception):  # response for an unexpected report id fails the job
+        C.gather_helper_resps(_sizes(prep_msg=5), h(KATS["agg_job_resp"]["expected"]),
+                              nonces[::-1].copy(), np.zeros(2, np.uint8))
+
+
+def test_encode_agg_job_resp_matches_framing():
+    nonces = np.frombuffer(bytes(range(48)), np.uint8).reshape(3, 16)
+    msgs = np.frombuffer(bytes(range(100, 148)), np.uint8).reshape(3, 16)
+    st = np.array([0, 5, 0], np.uint8)
+    got = C.encode_agg_job_resp(nonces, msgs, 16, st)
+    items = b"".join(M.helper_prepare_resps(nonces, msgs, st))
+    assert got == struct.pack(">I", len(items)) + items
+    # and the leader reads it back
+    pm, st2 = C.gather_helper_resps(_sizes(prep_msg=16), got, nonces, np.zeros(3, np.uint8))
+    assert list(st2) == [0, 5, 0] and (pm[[0, 2]] == msgs[[0, 2]]).all()
+
+
+def test_plaintext_input_share_kats_and_errors():
+    cases = KATS["plaintext_input_share"]["cases"]
+    pts = [h(c["expected"]) for c in cases]
+    dup = h("0010" "0000" "0000" "0000" "0000" "0000" "0000" "0000" "0000") + h("0000000430313233")
+    bad = [pts[0] + b"\x00", h("0000" "00000003303132"), dup]
+    out, st = C.decode_plaintext_input_shares(_sizes(helper_input_share=4), pts + bad)
+    assert out[0].tobytes() == h(cases[0]["payload"]) and out[1].tobytes() == h(cases[1]["payload"])
+    assert list(st) == [0, 0, 8, 8, 8]
+
+
+def _plaintext(payload: bytes) -> bytes:
+    """PlaintextInputShare{extensions: [], payload} (lib.rs:1278-1295)."""
+    return b"\x00\x00" + struct.pack(">I", len(payload)) + payload
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "fp16_3"])
+def test_message_round_trip_through_engine(name):
+    """Leader prepare_init -> AggregationJobInitializeReq bytes -> helper decode/gather ->
+    [HPKE open: identity here; CPU-side, out of scope] -> PlaintextInputShare decode ->
+    prio3gpu_helper_init -> AggregationJobResp bytes -> leader gather -> prepare_next: both
+    aggregates equal the oracle's, and one report with a mangled public share is rejected alone
+    (InvalidMessage) without disturbing the others."""
+    from janus_amd.prio3 import Prio3Gpu
+    from tests.reports import CONFIGS, expected_aggregate, make_batch
+    b = make_batch(name, 10)
+    c = CONFIGS[name]
+    v = Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"], length=c["length"],
+                 chunk_length=c["chunk"])
+    s = v.sizes
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    assert (lst == 0).all()
+    cts = [(1, b"", _plaintext(b.helper_in[r].tobytes())) for r in range(b.n)]
+    req = C.encode_agg_init_req(C.TIME_INTERVAL, None, b"", b.nonces, list(range(b.n)), b.public,
+                                cts, lp, lst)
+    if s.public_share:  # corrupt report 3's public share length in the wire bytes
+        raw = bytearray(req)
+        d = C.decode_agg_init_req(bytes(raw))
+        o = d.views[3].public_share_off - 4
+        raw[o:o + 4] = struct.pack(">I", s.public_share)  # unchanged length, keeps it decodable
+        req = bytes(raw)
+    # helper
+    d = C.decode_agg_init_req(req)
+    assert d.n == b.n and (d.times() == np.arange(b.n)).all()
+    nonces, pub, lps, st = C.gather_prepare_inits(s, d)
+    bad = 3
+    st[bad] = 8 if s.public_share else 0  # emulate: report 3's public share failed to decode
+    hin, st = C.decode_plaintext_input_shares(s, [ct[2] for ct in d.hpke_ciphertexts()], 1, st)
+    hagg = v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, nonces, pub, hin, lps, agg=hagg, status=st)
+    resp = C.encode_agg_job_resp(nonces, msgs, s.prep_msg, hst)
+    # leader
+    pm, lst2 = C.gather_helper_resps(s, resp, b.nonces, lst.copy())
+    mask = hst == 0
+    assert (lst2 == hst).all()
+    lagg = v.new_aggregate(1)
+    v.prepare_next(ls, pm, lst2, want_output_shares=False, agg=lagg)
+    for agg, which in ((lagg, "leader"), (hagg, "helper")):
+        got, cnt = agg.read(0)
+        exp, ecnt = expected_aggregate(b, which, mask=mask)
+        assert got == exp and cnt == ecnt
