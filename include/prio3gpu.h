@@ -127,6 +127,14 @@ int prio3gpu_agg_read(prio3gpu_agg* agg, uint32_t slot, uint8_t* out_share, uint
 int prio3gpu_agg_merge_bytes(prio3gpu_agg* agg, uint32_t slot, const uint8_t* share,
                              uint64_t count);
 
+/* Collector::unshard (collector/src/lib.rs:539): sum `num_shares` aggregate shares
+ * (num_shares x aggregate_share bytes, host) mod p and decode the aggregate result:
+ *   Count / Sum / SumVec / Histogram -> out_u128: output_len x 16-byte LE integers;
+ *   FixedPoint vectors               -> out_f64:  d * 2^(1-bits) - num_measurements per entry
+ *                                                 (prio to_float_bits; interop FP16 KAT). */
+int prio3gpu_unshard(const prio3gpu_ctx* ctx, const uint8_t* agg_shares, size_t num_shares,
+                     uint64_t num_measurements, uint8_t* out_u128, double* out_f64);
+
 /* prepare_init for n reports with the state's agg_id (0 = leader, 1 = helper).
  *   nonces          n x 16          (report IDs)
  *   public_shares   n x public_share

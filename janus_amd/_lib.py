@@ -80,6 +80,7 @@ def _declare(lib):
         "prio3gpu_dev_free": (c.c_int, [P, P]),
         "prio3gpu_memcpy": (c.c_int, [P, P, P, c.c_size_t]),
         "prio3gpu_last_error": (c.c_char_p, []),
+        "prio3gpu_unshard": (c.c_int, [P, u8p, c.c_size_t, c.c_uint64, u8p, P]),
         # DAP codec edge (host-only, codec.cpp)
         "prio3gpu_decode_agg_init_req": (c.c_int, [u8p, c.c_size_t, c.c_int, u8p, P, P, c.c_size_t,
                                                    c.POINTER(c.c_size_t)]),
@@ -114,7 +115,7 @@ EXPORTED = [
     "prio3gpu_random_size", "prio3gpu_shard", "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
     "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
     "prio3gpu_prof_kernel_name", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
-    "prio3gpu_last_error", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
+    "prio3gpu_last_error", "prio3gpu_unshard", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
     "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",
     "prio3gpu_encode_agg_init_req", "prio3gpu_decode_agg_job_resp", "prio3gpu_gather_helper_resps",
 ]

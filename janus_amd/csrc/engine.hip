@@ -1036,6 +1036,45 @@ int prio3gpu_agg_read(prio3gpu_agg* a, uint32_t slot, uint8_t* out_share, uint64
   return 0;
 }
 
+// Collector::unshard (collector/src/lib.rs:539; prio Prio3::unshard): sum the aggregate shares
+// mod p, then decode_result: integers for Count/Sum/SumVec/Histogram (16-byte LE each), or
+// d * 2^(1-bits) - num_measurements per entry for the fixed-point vector (prio to_float_bits).
+int prio3gpu_unshard(const prio3gpu_ctx* c, const uint8_t* agg_shares, size_t num_shares,
+                     uint64_t num_measurements, uint8_t* out_u128, double* out_f64) {
+  if (!c || !agg_shares || num_shares == 0) {
+    set_err("unshard: bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  const Cfg& g = c->cfg;
+  const uint32_t es = g.es;
+  const u128 p = es == 16 ? P128 : P64;
+  const size_t share_len = (size_t)g.out_len * es;
+  const bool fp = g.kind == KIND_FPVEC;
+  if ((fp && !out_f64) || (!fp && !out_u128)) {
+    set_err("unshard: %s output required", fp ? "f64" : "u128");
+    return PRIO3GPU_E_ARG;
+  }
+  for (uint32_t e = 0; e < g.out_len; ++e) {
+    u128 acc = 0;
+    for (size_t k = 0; k < num_shares; ++k) {
+      u128 x = 0;
+      const uint8_t* src = agg_shares + k * share_len + (size_t)e * es;
+      for (uint32_t b = 0; b < es; ++b) x |= (u128)src[b] << (8 * b);
+      if (x >= p) {
+        set_err("unshard: aggregate share element out of range");
+        return PRIO3GPU_E_ARG;
+      }
+      acc = addmod(acc, x, p);
+    }
+    if (fp) {
+      out_f64[e] = std::ldexp((double)acc, 1 - (int)g.bits) - (double)num_measurements;
+    } else {
+      for (uint32_t b = 0; b < 16; ++b) out_u128[(size_t)e * 16 + b] = (uint8_t)(acc >> (8 * b));
+    }
+  }
+  return 0;
+}
+
 int prio3gpu_agg_merge_bytes(prio3gpu_agg* a, uint32_t slot, const uint8_t* share,
                              uint64_t count) {
   if (!a || slot >= a->slots || !share) {

@@ -309,19 +309,28 @@ class Prio3Gpu:
         return [int.from_bytes(b[i:i + es], "little") for i in range(0, len(b), es)]
 
     def unshard(self, aggregate_shares: Sequence[bytes], num_measurements: int = None):
-        """`Collector::unshard` (collector/src/lib.rs:539): sum the aggregate shares and decode the
-        result.  Fixed-point vectors decode each sum d of `num_measurements` encoded entries as
-        d * 2^(1-bits) - num_measurements (prio `to_float_bits`)."""
-        p = self.modulus
-        vecs = [self.decode_field_vec(a) for a in aggregate_shares]
-        out = [sum(col) % p for col in zip(*vecs)]
-        if self.kind in (COUNT, SUM):
-            return out[0]
+        """`Collector::unshard` (collector/src/lib.rs:539) via prio3gpu_unshard: sum the aggregate
+        shares mod p and decode the result (integers; fixed-point vectors decode each sum d of
+        `num_measurements` encoded entries as d * 2^(1-bits) - num_measurements)."""
+        s = self.sizes
+        shares = b"".join(bytes(a) for a in aggregate_shares)
+        if len(shares) != len(aggregate_shares) * s.aggregate_share or not aggregate_shares:
+            raise ValueError("aggregate shares must be aggregate_share bytes each")
+        buf = np.frombuffer(shares, np.uint8).copy()
         if self.kind == FPVEC:
             if num_measurements is None:
                 raise ValueError("fixed-point unshard needs the report count")
-            return [float(d) * 2.0 ** (1 - self.bits) - num_measurements for d in out]
-        return out
+            out = np.zeros(s.output_len, np.float64)
+            check(lib().prio3gpu_unshard(self._ctx, _ptr(buf), len(aggregate_shares),
+                                         num_measurements, None, _ptr(out)), "unshard")
+            return [float(x) for x in out]
+        out = np.zeros((s.output_len, 16), np.uint8)
+        check(lib().prio3gpu_unshard(self._ctx, _ptr(buf), len(aggregate_shares),
+                                     num_measurements or 0, _ptr(out), None), "unshard")
+        vals = [int.from_bytes(out[e].tobytes(), "little") for e in range(s.output_len)]
+        if self.kind in (COUNT, SUM):
+            return vals[0]
+        return vals
 
 
 class Comm:
