@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--workers", type=int, default=1,
                     help="concurrent aggregation-job workers per GPU, one engine context (HIP "
@@ -336,6 +337,41 @@ def main():
                          f"prepare+aggregate, {nthr} threads, {cpu_s:.1f} s; C restatement of "
                          f"prio 0.15.1 (reference not buildable)"}
 
+    # ---- HPKE open on host threads (excluded from `value`, reported separately: SURVEY §8(d)) --
+    hpke_rep = None
+    if rank == 0 and world == 1 and args.hpke:
+        from janus_amd import codec as C
+        from janus_amd import hpke as H
+        nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        nh = min(U, 8192)
+        kp = H.generate_hpke_config_and_private_key(1)
+        info = H.application_info(H.Label.INPUT_SHARE, H.ROLE_CLIENT, H.ROLE_HELPER)
+        hn = d_nonces[:nh].cpu().numpy()
+        hp = d_pub[:nh].cpu().numpy() if d_pub is not None else np.zeros((nh, 0), np.uint8)
+        hh = d_hin[:nh].cpu().numpy()
+        task_id = bytes(32)
+        cts = [H.seal(kp.config, info, b"\0\0" + len(hh[i]).to_bytes(4, "big") + hh[i].tobytes(),
+                      H.input_share_aad(task_id, hn[i].tobytes(), 0, hp[i].tobytes()))
+               for i in range(nh)]
+        req = C.decode_agg_init_req(C.encode_agg_init_req(
+            C.TIME_INTERVAL, None, b"", hn, [0] * nh, hp, cts, np.zeros((nh, s.prep_share), np.uint8)))
+        H.open_report_shares(task_id, req, [kp], [], None, nthr)  # warm
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            pts, offs, hst = H.open_report_shares(task_id, req, [kp], [], None, nthr)
+            reps += 1
+            if time.perf_counter() - t0 > 2.0:
+                break
+        hs_dt = time.perf_counter() - t0
+        assert (hst == 0).all()
+        hin2, hst = C.decode_plaintext_input_shares_raw(s, pts, offs, 1, hst)
+        assert (hst == 0).all() and np.array_equal(hin2, hh)
+        hpke_rep = {"value": round(reps * nh / hs_dt, 1), "unit": "helper input shares opened/s",
+                    "threads": nthr, "suite": "X25519HkdfSha256/HkdfSha256/Aes128Gcm",
+                    "sample": f"{nh} helper input shares x {reps}",
+                    "note": "CPU stage in front of the GPU path (north star); not in `value`"}
+
     out = {
         "metric": METRIC if args.config == "sumvec" else f"reports/sec prepared+aggregated, {label}",
         "value": round(value, 2),
@@ -355,6 +391,7 @@ def main():
                                   f"RCCL all-gather merge"},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "hpke_open": hpke_rep,
         "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
         "parity": parity,
         "gen_seconds": round(gen_s, 1),

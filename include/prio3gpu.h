@@ -66,6 +66,8 @@ enum prio3gpu_kind {
 
 enum prio3gpu_status {
   PRIO3GPU_OK = 0,
+  PRIO3GPU_HPKE_UNKNOWN_CONFIG_ID = 3,
+  PRIO3GPU_HPKE_DECRYPT_ERROR = 4,
   PRIO3GPU_VDAF_PREP_ERROR = 5,
   PRIO3GPU_INVALID_MESSAGE = 8
 };
@@ -75,7 +77,9 @@ enum prio3gpu_err {
   PRIO3GPU_E_ARG = -1,
   PRIO3GPU_E_HIP = -2,
   PRIO3GPU_E_RCCL = -3,
-  PRIO3GPU_E_CAPACITY = -4
+  PRIO3GPU_E_CAPACITY = -4,
+  PRIO3GPU_E_HPKE = -5,        /* HPKE open/seal failed (bad key, tag mismatch) */
+  PRIO3GPU_E_UNSUPPORTED = -6  /* HPKE suite not supported */
 };
 
 typedef struct prio3gpu_ctx prio3gpu_ctx;
@@ -287,6 +291,54 @@ int prio3gpu_gather_helper_resps(const prio3gpu_sizes* sizes, const uint8_t* msg
                                  const prio3gpu_prepare_resp_view* views, size_t n_views,
                                  const uint8_t* nonces, size_t n, uint8_t* prep_msgs,
                                  uint8_t* status);
+
+/* ---- HPKE open on host threads (janus_amd/csrc/hpke.cpp) -------------------
+ * RFC 9180 base mode, single shot, as core/src/hpke.rs:158-202 (hpke::seal / hpke::open).
+ * Suites: KEM 0x20 X25519HkdfSha256 | 0x10 P256HkdfSha256; KDF 1/2/3 HkdfSha256/384/512;
+ * AEAD 1/2/3 Aes128Gcm/Aes256Gcm/ChaCha20Poly1305.  Keys are the RFC 9180 serializations
+ * (X25519: 32 B; P-256: 32-B scalar, 65-B uncompressed point).
+ * Returns 0, PRIO3GPU_E_HPKE (decryption / key failure), PRIO3GPU_E_UNSUPPORTED (suite),
+ * PRIO3GPU_E_CAPACITY (out buffer too small; the needed length is stored), PRIO3GPU_E_ARG. */
+typedef struct prio3gpu_hpke_keypair {  /* HpkeKeypair (core/src/hpke.rs:233-255) */
+  uint8_t config_id;
+  uint16_t kem_id, kdf_id, aead_id;
+  const uint8_t* public_key;
+  uint32_t public_key_len;
+  const uint8_t* private_key;
+  uint32_t private_key_len;
+} prio3gpu_hpke_keypair;
+
+int prio3gpu_hpke_open(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id, const uint8_t* sk,
+                       size_t sk_len, const uint8_t* pk, size_t pk_len, const uint8_t* enc,
+                       size_t enc_len, const uint8_t* info, size_t info_len, const uint8_t* aad,
+                       size_t aad_len, const uint8_t* ct, size_t ct_len, uint8_t* pt, size_t cap,
+                       size_t* pt_len);
+/* sk_e = ephemeral private key (NULL: fresh random; fixed keys are for tests). */
+int prio3gpu_hpke_seal(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id, const uint8_t* pk,
+                       size_t pk_len, const uint8_t* sk_e, size_t sk_e_len, const uint8_t* info,
+                       size_t info_len, const uint8_t* aad, size_t aad_len, const uint8_t* pt,
+                       size_t pt_len, uint8_t* enc, size_t enc_cap, size_t* enc_len, uint8_t* ct,
+                       size_t ct_cap, size_t* ct_len);
+/* SerializePublicKey(pk(sk)) -- key generation (generate_hpke_config_and_private_key,
+ * core/src/hpke.rs:204-231); PRIO3GPU_E_HPKE if sk is not a valid private key. */
+int prio3gpu_hpke_public_key(uint16_t kem_id, const uint8_t* sk, size_t sk_len, uint8_t* pk,
+                             size_t cap, size_t* pk_len);
+/* Helper: open the n encrypted input shares of a decoded AggregationJobInitializeReq on
+ * `threads` host threads (<= 0: all cores), replacing the per-report hpke::open of
+ * aggregator.rs:1634-1700: keypair by config id (task keys first, global keys on decryption
+ * failure), info = "dap-07 input share" || sender_role || recipient_role, aad = InputShareAad
+ * (task_id[32], report metadata, public share).  Unknown config id -> status 3
+ * (HpkeUnknownConfigId), failure -> 4 (HpkeDecryptError); reports with status != 0 on entry are
+ * skipped.  offsets (n + 1) are always filled: report i's plaintext (a PlaintextInputShare for
+ * prio3gpu_decode_plaintext_input_shares) is plaintexts[offsets[i] .. offsets[i+1]);
+ * plaintexts == NULL is a sizing call. */
+int prio3gpu_hpke_open_report_shares(const uint8_t* task_id, const prio3gpu_hpke_keypair* task_keys,
+                                     size_t n_task_keys, const prio3gpu_hpke_keypair* global_keys,
+                                     size_t n_global_keys, uint8_t sender_role,
+                                     uint8_t recipient_role, const uint8_t* msg,
+                                     const prio3gpu_prepare_init_view* views, size_t n,
+                                     uint8_t* plaintexts, uint64_t* offsets, uint8_t* status,
+                                     int threads);
 
 /* Last error message for this thread (static storage). */
 const char* prio3gpu_last_error(void);

@@ -28,7 +28,7 @@ class Prio3GpuError(RuntimeError):
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP engine for gfx950 into janus_amd/lib/libprio3gpu.so."""
-    srcs = [CSRC / "engine.hip", CSRC / "codec.cpp"]
+    srcs = [CSRC / "engine.hip", CSRC / "codec.cpp", CSRC / "hpke.cpp"]
     deps = srcs + list(CSRC.glob("*.h")) + [INCLUDE / "prio3gpu.h"]
     if LIB_PATH.exists() and not force:
         newest = max(p.stat().st_mtime for p in deps)
@@ -37,7 +37,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     LIB_DIR.mkdir(exist_ok=True)
     tmp = LIB_PATH.with_suffix(".so.tmp")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", str(tmp)] + [str(x) for x in srcs] + ["-lrccl"]
+           "-o", str(tmp)] + [str(x) for x in srcs] + ["-lrccl", "-lcrypto"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -97,6 +97,20 @@ def _declare(lib):
                                                    c.POINTER(c.c_size_t)]),
         "prio3gpu_gather_helper_resps": (c.c_int, [P, u8p, P, c.c_size_t, u8p, c.c_size_t, u8p,
                                                    u8p]),
+        # HPKE on host threads (hpke.cpp)
+        "prio3gpu_hpke_open": (c.c_int, [c.c_uint16, c.c_uint16, c.c_uint16, u8p, c.c_size_t, u8p,
+                                         c.c_size_t, u8p, c.c_size_t, u8p, c.c_size_t, u8p,
+                                         c.c_size_t, u8p, c.c_size_t, u8p, c.c_size_t,
+                                         c.POINTER(c.c_size_t)]),
+        "prio3gpu_hpke_seal": (c.c_int, [c.c_uint16, c.c_uint16, c.c_uint16, u8p, c.c_size_t, u8p,
+                                         c.c_size_t, u8p, c.c_size_t, u8p, c.c_size_t, u8p,
+                                         c.c_size_t, u8p, c.c_size_t, c.POINTER(c.c_size_t), u8p,
+                                         c.c_size_t, c.POINTER(c.c_size_t)]),
+        "prio3gpu_hpke_public_key": (c.c_int, [c.c_uint16, u8p, c.c_size_t, u8p, c.c_size_t,
+                                               c.POINTER(c.c_size_t)]),
+        "prio3gpu_hpke_open_report_shares": (c.c_int, [u8p, P, c.c_size_t, P, c.c_size_t,
+                                                       c.c_uint8, c.c_uint8, u8p, P, c.c_size_t,
+                                                       u8p, P, u8p, c.c_int]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(lib, name)
@@ -118,6 +132,8 @@ EXPORTED = [
     "prio3gpu_last_error", "prio3gpu_unshard", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
     "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",
     "prio3gpu_encode_agg_init_req", "prio3gpu_decode_agg_job_resp", "prio3gpu_gather_helper_resps",
+    "prio3gpu_hpke_open", "prio3gpu_hpke_seal", "prio3gpu_hpke_public_key",
+    "prio3gpu_hpke_open_report_shares",
 ]
 
 

@@ -102,10 +102,18 @@ def decode_plaintext_input_shares(sizes, plaintexts: Sequence[bytes], agg_id: in
                                   status: Optional[np.ndarray] = None):
     """HPKE-opened PlaintextInputShares -> (n, input share) array + status."""
     n = len(plaintexts)
-    st = np.zeros(n, np.uint8) if status is None else status
     offs = np.zeros(n + 1, np.uint64)
     offs[1:] = np.cumsum([len(p) for p in plaintexts])
     buf = np.frombuffer(b"".join(plaintexts) or b"\0", np.uint8).copy()
+    return decode_plaintext_input_shares_raw(sizes, buf, offs, agg_id, status)
+
+
+def decode_plaintext_input_shares_raw(sizes, buf: np.ndarray, offs: np.ndarray, agg_id: int = 1,
+                                      status: Optional[np.ndarray] = None):
+    """As decode_plaintext_input_shares, over one buffer + (n + 1) offsets (the layout
+    hpke.open_report_shares produces)."""
+    n = len(offs) - 1
+    st = np.zeros(n, np.uint8) if status is None else status
     w = sizes.leader_input_share if agg_id == 0 else sizes.helper_input_share
     out = np.zeros((n, w), np.uint8)
     check(lib().prio3gpu_decode_plaintext_input_shares(ctypes.byref(sizes), _p(buf), _p(offs), n,

@@ -1,0 +1,564 @@
+// HPKE (RFC 9180, base mode, single shot) for the helper's aggregate-init input shares, on CPU
+// threads in front of the codec edge (the north star keeps HPKE open on the
+// host).  Host code, part of libprio3gpu.so, built on the image's OpenSSL 3.0 libcrypto
+// primitives (X25519 / P-256 ECDH, SHA-2, AES-GCM, ChaCha20-Poly1305); the HPKE construction
+// itself (DHKEM, labeled HKDF, key schedule) is written out here.
+//
+// Reference behaviour:
+//   hpke::open / hpke::seal                         core/src/hpke.rs:158-202 (hpke-dispatch crate,
+//                                                    base_mode_open / base_mode_seal)
+//   HpkeApplicationInfo = label || sender || recipient  core/src/hpke.rs:44-77
+//   supported suites: KEM X25519HkdfSha256 (0x20), P256HkdfSha256 (0x10); KDF HkdfSha256/384/512
+//     (1/2/3); AEAD Aes128Gcm / Aes256Gcm / ChaCha20Poly1305 (1/2/3)  messages/src/lib.rs (HpkeKemId,
+//     HpkeKdfId, HpkeAeadId); pinned by core/src/hpke.rs:539-615 (RFC 9180 test vectors)
+//   helper per-report open: keypair by config id from the task's keys, then the global keys;
+//     unknown id -> HpkeUnknownConfigId (3); the task key is tried first and the global key
+//     only after a decryption failure; any failure -> HpkeDecryptError (4)
+//                                                    aggregator/src/aggregator.rs:1634-1700
+//   InputShareAad = TaskId[32] || ReportMetadata{ReportId[16], Time u64 BE} ||
+//     u32-prefixed public share                      messages/src/lib.rs:1790-1827
+#include <openssl/bn.h>
+#include <openssl/ec.h>
+#include <openssl/evp.h>
+#include <openssl/obj_mac.h>
+#include <openssl/rand.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/prio3gpu.h"
+
+namespace {
+
+enum : uint16_t { KEM_P256 = 0x10, KEM_X25519 = 0x20 };
+enum : uint16_t { KDF_SHA256 = 1, KDF_SHA384 = 2, KDF_SHA512 = 3 };
+enum : uint16_t { AEAD_AES128GCM = 1, AEAD_AES256GCM = 2, AEAD_CHACHA20POLY1305 = 3 };
+constexpr size_t kTag = 16, kNonce = 12, kMaxHash = 64;
+
+struct Algs {
+  const EVP_MD* md[4] = {};          // by KDF id (1..3)
+  const EVP_CIPHER* aead[4] = {};    // by AEAD id (1..3)
+  EC_GROUP* p256 = nullptr;
+  bool ok = false;
+};
+
+// Fetched once: per-call implicit fetches are the slow part of OpenSSL 3 one-shot APIs.
+const Algs& algs() {
+  static Algs a;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    a.md[1] = EVP_MD_fetch(nullptr, "SHA256", nullptr);
+    a.md[2] = EVP_MD_fetch(nullptr, "SHA384", nullptr);
+    a.md[3] = EVP_MD_fetch(nullptr, "SHA512", nullptr);
+    a.aead[1] = EVP_CIPHER_fetch(nullptr, "AES-128-GCM", nullptr);
+    a.aead[2] = EVP_CIPHER_fetch(nullptr, "AES-256-GCM", nullptr);
+    a.aead[3] = EVP_CIPHER_fetch(nullptr, "ChaCha20-Poly1305", nullptr);
+    a.p256 = EC_GROUP_new_by_curve_name(NID_X9_62_prime256v1);
+    a.ok = a.md[1] && a.md[2] && a.md[3] && a.aead[1] && a.aead[2] && a.aead[3] && a.p256;
+  });
+  return a;
+}
+
+struct Suite {
+  uint16_t kem, kdf, aead;
+  size_t nsecret, nenc, npk, nsk;  // KEM sizes (RFC 9180 §7.1)
+  size_t nk;                       // AEAD key size
+  size_t nh;                       // KDF output size
+};
+
+bool suite_of(uint16_t kem, uint16_t kdf, uint16_t aead, Suite* s) {
+  s->kem = kem, s->kdf = kdf, s->aead = aead;
+  if (kem == KEM_X25519) { s->nsecret = 32; s->nenc = s->npk = 32; s->nsk = 32; }
+  else if (kem == KEM_P256) { s->nsecret = 32; s->nenc = s->npk = 65; s->nsk = 32; }
+  else return false;
+  if (kdf == KDF_SHA256) s->nh = 32;
+  else if (kdf == KDF_SHA384) s->nh = 48;
+  else if (kdf == KDF_SHA512) s->nh = 64;
+  else return false;
+  if (aead == AEAD_AES128GCM) s->nk = 16;
+  else if (aead == AEAD_AES256GCM || aead == AEAD_CHACHA20POLY1305) s->nk = 32;
+  else return false;
+  return algs().ok;
+}
+
+// ---- HMAC / HKDF over a pre-fetched digest -------------------------------------------------
+
+struct Bytes {
+  std::vector<uint8_t> v;
+  Bytes& add(const void* p, size_t n) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    v.insert(v.end(), b, b + n);
+    return *this;
+  }
+  Bytes& add(const char* s) { return add(s, strlen(s)); }
+  Bytes& u16(uint16_t x) {
+    uint8_t b[2] = {uint8_t(x >> 8), uint8_t(x)};
+    return add(b, 2);
+  }
+};
+
+bool hmac(const EVP_MD* md, const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
+          uint8_t* out) {
+  const size_t bs = EVP_MD_get_block_size(md), hl = EVP_MD_get_size(md);
+  uint8_t k0[128] = {0}, pad[128];
+  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  if (!c) return false;
+  bool ok = true;
+  if (klen > bs) {
+    unsigned int l = 0;
+    ok = EVP_DigestInit_ex(c, md, nullptr) && EVP_DigestUpdate(c, key, klen) &&
+         EVP_DigestFinal_ex(c, k0, &l);
+  } else if (klen) {
+    memcpy(k0, key, klen);
+  }
+  uint8_t inner[kMaxHash];
+  unsigned int l = 0;
+  for (size_t i = 0; i < bs; ++i) pad[i] = k0[i] ^ 0x36;
+  ok = ok && EVP_DigestInit_ex(c, md, nullptr) && EVP_DigestUpdate(c, pad, bs) &&
+       EVP_DigestUpdate(c, msg, mlen) && EVP_DigestFinal_ex(c, inner, &l);
+  for (size_t i = 0; i < bs; ++i) pad[i] = k0[i] ^ 0x5c;
+  ok = ok && EVP_DigestInit_ex(c, md, nullptr) && EVP_DigestUpdate(c, pad, bs) &&
+       EVP_DigestUpdate(c, inner, hl) && EVP_DigestFinal_ex(c, out, &l);
+  EVP_MD_CTX_free(c);
+  return ok;
+}
+
+// LabeledExtract(salt, label, ikm) = HMAC(salt, "HPKE-v1" || suite_id || label || ikm)  (§4)
+bool labeled_extract(const EVP_MD* md, const Bytes& suite_id, const uint8_t* salt, size_t slen,
+                     const char* label, const uint8_t* ikm, size_t ilen, uint8_t* prk) {
+  Bytes m;
+  m.add("HPKE-v1").add(suite_id.v.data(), suite_id.v.size()).add(label).add(ikm, ilen);
+  return hmac(md, salt, slen, m.v.data(), m.v.size(), prk);
+}
+
+// LabeledExpand(prk, label, info, L) = HKDF-Expand(prk, I2OSP(L,2) || "HPKE-v1" || suite_id ||
+// label || info, L)
+bool labeled_expand(const EVP_MD* md, const Bytes& suite_id, const uint8_t* prk, size_t plen,
+                    const char* label, const uint8_t* info, size_t ilen, size_t L, uint8_t* out) {
+  Bytes li;
+  li.u16(uint16_t(L)).add("HPKE-v1").add(suite_id.v.data(), suite_id.v.size()).add(label);
+  li.add(info, ilen);
+  const size_t hl = EVP_MD_get_size(md);
+  if (L > 255 * hl) return false;
+  uint8_t t[kMaxHash];
+  size_t tl = 0, done = 0;
+  for (uint8_t i = 1; done < L; ++i) {
+    Bytes m;
+    m.add(t, tl).add(li.v.data(), li.v.size()).add(&i, 1);
+    if (!hmac(md, prk, plen, m.v.data(), m.v.size(), t)) return false;
+    tl = hl;
+    const size_t c = std::min(hl, L - done);
+    memcpy(out + done, t, c);
+    done += c;
+  }
+  return true;
+}
+
+// ---- DHKEM (§4.1) --------------------------------------------------------------------------
+
+// X25519 (RFC 7748 §5), radix 2^51.  Written out rather than taken from EVP_PKEY: OpenSSL
+// 3.0's per-call key/ctx construction serialises threads on provider locks (measured: 8 threads
+// opened 1.6x what 1 thread did), which is the very scaling the batched open needs.
+typedef unsigned __int128 u128;
+constexpr uint64_t kM51 = (uint64_t(1) << 51) - 1;
+struct Fe { uint64_t v[5]; };
+
+inline void fe_load(Fe& h, const uint8_t* s) {
+  uint64_t w[4];
+  memcpy(w, s, 32);  // little-endian host
+  h.v[0] = w[0] & kM51;
+  h.v[1] = ((w[0] >> 51) | (w[1] << 13)) & kM51;
+  h.v[2] = ((w[1] >> 38) | (w[2] << 26)) & kM51;
+  h.v[3] = ((w[2] >> 25) | (w[3] << 39)) & kM51;
+  h.v[4] = (w[3] >> 12) & kM51;  // bit 255 masked (RFC 7748 §5)
+}
+
+inline void fe_carry(Fe& h, const u128 r[5]) {
+  u128 c = 0, t[5];
+  for (int i = 0; i < 5; ++i) {
+    t[i] = r[i] + c;
+    c = t[i] >> 51;
+    t[i] &= kM51;
+  }
+  const u128 t0 = t[0] + c * 19;
+  h.v[0] = uint64_t(t0 & kM51);
+  h.v[1] = uint64_t(t[1] + (t0 >> 51));
+  for (int i = 2; i < 5; ++i) h.v[i] = uint64_t(t[i]);
+}
+
+inline void fe_mul(Fe& h, const Fe& f, const Fe& g) {
+  const uint64_t* a = f.v;
+  const uint64_t* b = g.v;
+  const uint64_t b1 = 19 * b[1], b2 = 19 * b[2], b3 = 19 * b[3], b4 = 19 * b[4];
+  u128 r[5];
+  r[0] = (u128)a[0] * b[0] + (u128)a[1] * b4 + (u128)a[2] * b3 + (u128)a[3] * b2 + (u128)a[4] * b1;
+  r[1] = (u128)a[0] * b[1] + (u128)a[1] * b[0] + (u128)a[2] * b4 + (u128)a[3] * b3 + (u128)a[4] * b2;
+  r[2] = (u128)a[0] * b[2] + (u128)a[1] * b[1] + (u128)a[2] * b[0] + (u128)a[3] * b4 +
+         (u128)a[4] * b3;
+  r[3] = (u128)a[0] * b[3] + (u128)a[1] * b[2] + (u128)a[2] * b[1] + (u128)a[3] * b[0] +
+         (u128)a[4] * b4;
+  r[4] = (u128)a[0] * b[4] + (u128)a[1] * b[3] + (u128)a[2] * b[2] + (u128)a[3] * b[1] +
+         (u128)a[4] * b[0];
+  fe_carry(h, r);
+}
+
+inline void fe_mul_small(Fe& h, const Fe& f, uint64_t k) {
+  u128 r[5];
+  for (int i = 0; i < 5; ++i) r[i] = (u128)f.v[i] * k;
+  fe_carry(h, r);
+}
+
+inline void fe_add(Fe& h, const Fe& f, const Fe& g) {
+  for (int i = 0; i < 5; ++i) h.v[i] = f.v[i] + g.v[i];
+}
+
+// f - g with a 2p bias; g must be a multiplication output (limbs < 2^51 + 2^20).
+inline void fe_sub(Fe& h, const Fe& f, const Fe& g) {
+  h.v[0] = f.v[0] + 0xFFFFFFFFFFFDAull - g.v[0];
+  for (int i = 1; i < 5; ++i) h.v[i] = f.v[i] + 0xFFFFFFFFFFFFEull - g.v[i];
+}
+
+inline void fe_cswap(Fe& a, Fe& b, uint64_t swap) {
+  const uint64_t m = 0 - swap;
+  for (int i = 0; i < 5; ++i) {
+    const uint64_t t = m & (a.v[i] ^ b.v[i]);
+    a.v[i] ^= t;
+    b.v[i] ^= t;
+  }
+}
+
+void fe_store(uint8_t* s, const Fe& f) {
+  Fe h = f;
+  for (int pass = 0; pass < 2; ++pass) {
+    uint64_t c = 0;
+    for (int i = 0; i < 5; ++i) {
+      h.v[i] += c;
+      c = h.v[i] >> 51;
+      h.v[i] &= kM51;
+    }
+    h.v[0] += 19 * c;
+  }
+  uint64_t q = (h.v[0] + 19) >> 51;  // q = 1 iff h >= p
+  for (int i = 1; i < 5; ++i) q = (h.v[i] + q) >> 51;
+  h.v[0] += 19 * q;
+  uint64_t c = 0;
+  for (int i = 0; i < 5; ++i) {
+    h.v[i] += c;
+    c = h.v[i] >> 51;
+    h.v[i] &= kM51;
+  }
+  const uint64_t w[4] = {h.v[0] | (h.v[1] << 51), (h.v[1] >> 13) | (h.v[2] << 38),
+                         (h.v[2] >> 26) | (h.v[3] << 25), (h.v[3] >> 39) | (h.v[4] << 12)};
+  memcpy(s, w, 32);
+}
+
+void x25519(uint8_t* out, const uint8_t* scalar, const uint8_t* point) {
+  uint8_t k[32];
+  memcpy(k, scalar, 32);
+  k[0] &= 248;  // decodeScalar25519
+  k[31] &= 127;
+  k[31] |= 64;
+  Fe x1, x2 = {{1, 0, 0, 0, 0}}, z2 = {{0, 0, 0, 0, 0}}, x3, z3 = {{1, 0, 0, 0, 0}};
+  fe_load(x1, point);
+  x3 = x1;
+  uint64_t swap = 0;
+  for (int t = 254; t >= 0; --t) {
+    const uint64_t kt = (k[t >> 3] >> (t & 7)) & 1;
+    swap ^= kt;
+    fe_cswap(x2, x3, swap);
+    fe_cswap(z2, z3, swap);
+    swap = kt;
+    Fe A, AA, B, BB, E, C, D, DA, CB, t0, t1;
+    fe_add(A, x2, z2);
+    fe_mul(AA, A, A);
+    fe_sub(B, x2, z2);
+    fe_mul(BB, B, B);
+    fe_sub(E, AA, BB);
+    fe_add(C, x3, z3);
+    fe_sub(D, x3, z3);
+    fe_mul(DA, D, A);
+    fe_mul(CB, C, B);
+    fe_add(t0, DA, CB);
+    fe_mul(x3, t0, t0);
+    fe_sub(t1, DA, CB);
+    fe_mul(t1, t1, t1);
+    fe_mul(z3, x1, t1);
+    fe_mul(x2, AA, BB);
+    fe_mul_small(t0, E, 121665);
+    fe_add(t0, AA, t0);
+    fe_mul(z2, E, t0);
+  }
+  fe_cswap(x2, x3, swap);
+  fe_cswap(z2, z3, swap);
+  // z2^(p-2), p - 2 = 2^255 - 21: every bit of 0..254 set except bits 2 and 4
+  Fe r = {{1, 0, 0, 0, 0}};
+  for (int i = 254; i >= 0; --i) {
+    fe_mul(r, r, r);
+    if (i != 2 && i != 4) fe_mul(r, r, z2);
+  }
+  fe_mul(x2, x2, r);
+  fe_store(out, x2);
+}
+
+bool x25519_dh(const uint8_t* sk, const uint8_t* pk, uint8_t* dh) {
+  x25519(dh, sk, pk);
+  uint8_t acc = 0;  // RFC 9180 §7.1.4: an all-zero X25519 output is an error
+  for (int i = 0; i < 32; ++i) acc |= dh[i];
+  return acc != 0;
+}
+
+bool x25519_public(const uint8_t* sk, uint8_t* pk) {
+  static const uint8_t kBase[32] = {9};
+  x25519(pk, sk, kBase);
+  return true;
+}
+
+// P-256: sk is a 32-byte big-endian scalar in [1, n); public keys are uncompressed points (65 B,
+// on-curve check in oct2point); the DH output is the x coordinate (32 B).
+bool p256_mul(const uint8_t* sk, const uint8_t* pk /* nullptr = generator */, uint8_t* out,
+              size_t out_len) {
+  const EC_GROUP* g = algs().p256;
+  BN_CTX* bc = BN_CTX_new();
+  BIGNUM* k = BN_bin2bn(sk, 32, nullptr);
+  EC_POINT* P = pk ? EC_POINT_new(g) : nullptr;
+  EC_POINT* R = EC_POINT_new(g);
+  bool ok = bc && k && R && !BN_is_zero(k) && BN_cmp(k, EC_GROUP_get0_order(g)) < 0;
+  if (ok && pk) ok = P && EC_POINT_oct2point(g, P, pk, 65, bc) == 1;
+  if (ok) ok = EC_POINT_mul(g, R, pk ? nullptr : k, pk ? P : nullptr, pk ? k : nullptr, bc) == 1;
+  if (ok) ok = !EC_POINT_is_at_infinity(g, R);
+  if (ok) {
+    if (out_len == 65) {
+      ok = EC_POINT_point2oct(g, R, POINT_CONVERSION_UNCOMPRESSED, out, 65, bc) == 65;
+    } else {
+      BIGNUM* x = BN_new();
+      ok = x && EC_POINT_get_affine_coordinates(g, R, x, nullptr, bc) == 1 &&
+           BN_bn2binpad(x, out, 32) == 32;
+      BN_free(x);
+    }
+  }
+  EC_POINT_free(R);
+  EC_POINT_free(P);
+  BN_clear_free(k);
+  BN_CTX_free(bc);
+  return ok;
+}
+
+bool dh(const Suite& s, const uint8_t* sk, const uint8_t* pk, uint8_t* out) {
+  return s.kem == KEM_X25519 ? x25519_dh(sk, pk, out) : p256_mul(sk, pk, out, 32);
+}
+
+bool public_of(const Suite& s, const uint8_t* sk, uint8_t* pk) {
+  return s.kem == KEM_X25519 ? x25519_public(sk, pk) : p256_mul(sk, nullptr, pk, 65);
+}
+
+// ExtractAndExpand(dh, enc || pkRm) with suite_id = "KEM" || I2OSP(kem_id, 2); the KEM's KDF is
+// HKDF-SHA256 for both supported KEMs.
+bool kem_shared_secret(const Suite& s, const uint8_t* dhv, const uint8_t* enc, const uint8_t* pkR,
+                       uint8_t* ss) {
+  const EVP_MD* md = algs().md[KDF_SHA256];
+  Bytes sid;
+  sid.add("KEM").u16(s.kem);
+  uint8_t prk[kMaxHash];
+  if (!labeled_extract(md, sid, nullptr, 0, "eae_prk", dhv, 32, prk)) return false;
+  Bytes ctx;
+  ctx.add(enc, s.nenc).add(pkR, s.npk);
+  return labeled_expand(md, sid, prk, 32, "shared_secret", ctx.v.data(), ctx.v.size(), s.nsecret,
+                        ss);
+}
+
+// KeySchedule(mode_base, shared_secret, info, "", "") -> (key, base_nonce)  (§5.1)
+bool key_schedule(const Suite& s, const uint8_t* ss, const uint8_t* info, size_t ilen,
+                  uint8_t* key, uint8_t* nonce) {
+  const EVP_MD* md = algs().md[s.kdf];
+  Bytes sid;
+  sid.add("HPKE").u16(s.kem).u16(s.kdf).u16(s.aead);
+  uint8_t psk_id_hash[kMaxHash], info_hash[kMaxHash], secret[kMaxHash];
+  if (!labeled_extract(md, sid, nullptr, 0, "psk_id_hash", nullptr, 0, psk_id_hash) ||
+      !labeled_extract(md, sid, nullptr, 0, "info_hash", info, ilen, info_hash) ||
+      !labeled_extract(md, sid, ss, s.nsecret, "secret", nullptr, 0, secret))
+    return false;
+  Bytes ksc;
+  const uint8_t mode = 0;
+  ksc.add(&mode, 1).add(psk_id_hash, s.nh).add(info_hash, s.nh);
+  return labeled_expand(md, sid, secret, s.nh, "key", ksc.v.data(), ksc.v.size(), s.nk, key) &&
+         labeled_expand(md, sid, secret, s.nh, "base_nonce", ksc.v.data(), ksc.v.size(), kNonce,
+                        nonce);
+}
+
+bool aead(const Suite& s, bool encrypt, const uint8_t* key, const uint8_t* nonce,
+          const uint8_t* aad, size_t alen, const uint8_t* in, size_t inlen, uint8_t* out) {
+  // encrypt: in = plaintext (inlen), out = ciphertext || tag;  decrypt: in = ct || tag.
+  if (!encrypt && inlen < kTag) return false;
+  const size_t body = encrypt ? inlen : inlen - kTag;
+  EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
+  int l = 0;
+  bool ok = c && EVP_CipherInit_ex2(c, algs().aead[s.aead], key, nonce, encrypt ? 1 : 0,
+                                    nullptr) == 1;
+  if (ok && alen) ok = EVP_CipherUpdate(c, nullptr, &l, aad, int(alen)) == 1;
+  if (ok && body) ok = EVP_CipherUpdate(c, out, &l, in, int(body)) == 1;
+  if (ok && !encrypt)
+    ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_AEAD_SET_TAG, int(kTag),
+                             const_cast<uint8_t*>(in + body)) == 1;
+  uint8_t fin[16];
+  if (ok) ok = EVP_CipherFinal_ex(c, fin, &l) == 1;
+  if (ok && encrypt) ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_AEAD_GET_TAG, int(kTag), out + body) == 1;
+  EVP_CIPHER_CTX_free(c);
+  return ok;
+}
+
+int open_one(const Suite& s, const uint8_t* skR, size_t sk_len, const uint8_t* pkR, size_t pk_len,
+             const uint8_t* enc, size_t enc_len, const uint8_t* info, size_t ilen,
+             const uint8_t* aad, size_t alen, const uint8_t* ct, size_t ct_len, uint8_t* pt) {
+  if (sk_len != s.nsk || pk_len != s.npk) return PRIO3GPU_E_ARG;
+  if (enc_len != s.nenc || ct_len < kTag) return PRIO3GPU_E_HPKE;
+  uint8_t dhv[32], ss[32], key[32], nonce[kNonce];
+  if (!dh(s, skR, enc, dhv) || !kem_shared_secret(s, dhv, enc, pkR, ss) ||
+      !key_schedule(s, ss, info, ilen, key, nonce) ||
+      !aead(s, false, key, nonce, aad, alen, ct, ct_len, pt))
+    return PRIO3GPU_E_HPKE;
+  return 0;
+}
+
+// parallel_for over [0, n) on `threads` host threads (chunks of 8 reports).
+template <class F>
+void parallel_for(size_t n, int threads, F&& f) {
+  size_t t = threads > 0 ? size_t(threads) : std::max(1u, std::thread::hardware_concurrency());
+  t = std::min(t, (n + 7) / 8);
+  if (t <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (;;) {
+      const size_t b = next.fetch_add(8);
+      if (b >= n) return;
+      for (size_t i = b; i < std::min(n, b + 8); ++i) f(i);
+    }
+  };
+  std::vector<std::thread> pool;
+  for (size_t k = 1; k < t; ++k) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int prio3gpu_hpke_open(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id, const uint8_t* sk,
+                       size_t sk_len, const uint8_t* pk, size_t pk_len, const uint8_t* enc,
+                       size_t enc_len, const uint8_t* info, size_t info_len, const uint8_t* aad,
+                       size_t aad_len, const uint8_t* ct, size_t ct_len, uint8_t* pt, size_t cap,
+                       size_t* pt_len) {
+  Suite s;
+  if (!suite_of(kem_id, kdf_id, aead_id, &s)) return PRIO3GPU_E_UNSUPPORTED;
+  if (!sk || !pk || !enc || !ct || !pt_len) return PRIO3GPU_E_ARG;
+  if (ct_len < kTag) return PRIO3GPU_E_HPKE;
+  *pt_len = ct_len - kTag;
+  if (!pt || cap < ct_len - kTag) return PRIO3GPU_E_CAPACITY;
+  return open_one(s, sk, sk_len, pk, pk_len, enc, enc_len, info, info_len, aad, aad_len, ct,
+                  ct_len, pt);
+}
+
+int prio3gpu_hpke_seal(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id, const uint8_t* pk,
+                       size_t pk_len, const uint8_t* sk_e, size_t sk_e_len, const uint8_t* info,
+                       size_t info_len, const uint8_t* aad, size_t aad_len, const uint8_t* pt,
+                       size_t pt_len, uint8_t* enc, size_t enc_cap, size_t* enc_len, uint8_t* ct,
+                       size_t ct_cap, size_t* ct_len) {
+  Suite s;
+  if (!suite_of(kem_id, kdf_id, aead_id, &s)) return PRIO3GPU_E_UNSUPPORTED;
+  if (!pk || !enc_len || !ct_len || (pt_len && !pt)) return PRIO3GPU_E_ARG;
+  *enc_len = s.nenc;
+  *ct_len = pt_len + kTag;
+  if (!enc || !ct || enc_cap < s.nenc || ct_cap < pt_len + kTag) return PRIO3GPU_E_CAPACITY;
+  if (pk_len != s.npk) return PRIO3GPU_E_ARG;
+  uint8_t ske[32];
+  if (sk_e) {
+    if (sk_e_len != s.nsk) return PRIO3GPU_E_ARG;
+    memcpy(ske, sk_e, 32);
+  } else {  // fresh ephemeral key (P-256: retry until the scalar is in [1, n))
+    for (int tries = 0;; ++tries) {
+      if (tries > 64 || RAND_bytes(ske, 32) != 1) return PRIO3GPU_E_HPKE;
+      if (s.kem == KEM_X25519 || public_of(s, ske, enc)) break;
+    }
+  }
+  uint8_t dhv[32], ss[32], key[32], nonce[kNonce];
+  if (!public_of(s, ske, enc) || !dh(s, ske, pk, dhv) || !kem_shared_secret(s, dhv, enc, pk, ss) ||
+      !key_schedule(s, ss, info, info_len, key, nonce) ||
+      !aead(s, true, key, nonce, aad, aad_len, pt, pt_len, ct))
+    return PRIO3GPU_E_HPKE;
+  return 0;
+}
+
+int prio3gpu_hpke_public_key(uint16_t kem_id, const uint8_t* sk, size_t sk_len, uint8_t* pk,
+                             size_t cap, size_t* pk_len) {
+  Suite s;
+  if (!suite_of(kem_id, KDF_SHA256, AEAD_AES128GCM, &s)) return PRIO3GPU_E_UNSUPPORTED;
+  if (!sk || !pk_len) return PRIO3GPU_E_ARG;
+  *pk_len = s.npk;
+  if (!pk || cap < s.npk) return PRIO3GPU_E_CAPACITY;
+  if (sk_len != s.nsk) return PRIO3GPU_E_ARG;
+  return public_of(s, sk, pk) ? 0 : PRIO3GPU_E_HPKE;
+}
+
+int prio3gpu_hpke_open_report_shares(const uint8_t* task_id, const prio3gpu_hpke_keypair* task_keys,
+                                     size_t n_task_keys, const prio3gpu_hpke_keypair* global_keys,
+                                     size_t n_global_keys, uint8_t sender_role,
+                                     uint8_t recipient_role, const uint8_t* msg,
+                                     const prio3gpu_prepare_init_view* views, size_t n,
+                                     uint8_t* plaintexts, uint64_t* offsets, uint8_t* status,
+                                     int threads) {
+  if (!msg || (n && (!views || !offsets))) return PRIO3GPU_E_ARG;
+  offsets[0] = 0;
+  for (size_t i = 0; i < n; ++i)
+    offsets[i + 1] = offsets[i] + (views[i].payload_len >= kTag ? views[i].payload_len - kTag : 0);
+  if (!plaintexts) return 0;  // sizing call
+  if (!task_id || !status) return PRIO3GPU_E_ARG;
+  if (!algs().ok) return PRIO3GPU_E_UNSUPPORTED;
+  static const char kLabel[] = "dap-07 input share";  // Label::InputShare, hpke.rs:52-57
+  Bytes info;
+  info.add(kLabel).add(&sender_role, 1).add(&recipient_role, 1);
+  auto find = [](const prio3gpu_hpke_keypair* ks, size_t nk, uint8_t id) {
+    for (size_t k = 0; k < nk; ++k)
+      if (ks[k].config_id == id) return &ks[k];
+    return static_cast<const prio3gpu_hpke_keypair*>(nullptr);
+  };
+  parallel_for(n, threads, [&](size_t i) {
+    if (status[i]) return;
+    const prio3gpu_prepare_init_view& v = views[i];
+    const prio3gpu_hpke_keypair* tk = find(task_keys, n_task_keys, v.hpke_config_id);
+    const prio3gpu_hpke_keypair* gk = find(global_keys, n_global_keys, v.hpke_config_id);
+    if (!tk && !gk) {
+      status[i] = 3;  // PrepareError::HpkeUnknownConfigId
+      return;
+    }
+    Bytes aad;  // InputShareAad
+    uint8_t tbe[8];
+    for (int b = 0; b < 8; ++b) tbe[b] = uint8_t(v.time >> (56 - 8 * b));
+    const uint32_t pl = v.public_share_len;
+    const uint8_t plbe[4] = {uint8_t(pl >> 24), uint8_t(pl >> 16), uint8_t(pl >> 8), uint8_t(pl)};
+    aad.add(task_id, 32).add(msg + v.report_id_off, 16).add(tbe, 8).add(plbe, 4);
+    aad.add(msg + v.public_share_off, pl);
+    uint8_t* out = plaintexts + offsets[i];
+    auto try_open = [&](const prio3gpu_hpke_keypair* kp) -> int {
+      Suite s;
+      if (!suite_of(kp->kem_id, kp->kdf_id, kp->aead_id, &s)) return PRIO3GPU_E_UNSUPPORTED;
+      return open_one(s, kp->private_key, kp->private_key_len, kp->public_key,
+                      kp->public_key_len, msg + v.enc_off, v.enc_len, info.v.data(),
+                      info.v.size(), aad.v.data(), aad.v.size(), msg + v.payload_off,
+                      v.payload_len, out);
+    };
+    int rc = try_open(tk ? tk : gk);
+    if (rc == PRIO3GPU_E_HPKE && tk && gk) rc = try_open(gk);  // second trial on decrypt failure
+    if (rc != 0) status[i] = 4;  // PrepareError::HpkeDecryptError
+  });
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+"""Batched helper aggregate-init driver: the host-side mirror of Janus's
+`VdafOps::handle_aggregate_init_generic` (aggregator/src/aggregator.rs:1561-2045) for one task,
+minus the datastore transaction (out of scope).
+
+Per aggregation job (one AggregationJobInitializeReq):
+  1. decode the request and gather the engine inputs          codec.cpp   (aggregator.rs:1561-1612)
+  2. HPKE-open every encrypted input share on host threads    hpke.cpp    (aggregator.rs:1634-1700)
+  3. decode the PlaintextInputShares into the input-share array          (aggregator.rs:1702-1768)
+  4. prio3gpu_helper_init: prepare_init + decide + prepare_next + accumulate on the GPU
+                                                                          (aggregator.rs:1775-1819)
+  5. encode the AggregationJobResp                                        (aggregator.rs:1811-1848)
+
+`handle_jobs` pipelines a stream of jobs: while the GPU runs job k (step 4, the ctypes call
+releases the GIL and blocks on the engine's stream), a host worker thread runs steps 1-3 of job
+k + 1 -- the north star's "HPKE open stays on pipelined CPU threads".  Per-report errors keep the
+reference's mapping: status 3 HpkeUnknownConfigId, 4 HpkeDecryptError, 5 VdafPrepError,
+8 InvalidMessage, each rejecting that report alone.
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from . import codec as C
+from . import hpke
+from .prio3 import AggregateShares, Prio3Gpu
+
+
+@dataclass
+class _Opened:
+    n: int
+    nonces: np.ndarray
+    public: np.ndarray
+    leader_prep: np.ndarray
+    helper_in: np.ndarray
+    status: np.ndarray
+    slots: Optional[np.ndarray]
+
+
+class HelperAggregateInit:
+    def __init__(self, vdaf: Prio3Gpu, task_id: bytes, task_keys: Sequence[hpke.HpkeKeypair],
+                 global_keys: Sequence[hpke.HpkeKeypair] = (), query_type: int = C.TIME_INTERVAL,
+                 hpke_threads: int = 0,
+                 batch_slot_of: Optional[Callable[[np.ndarray], np.ndarray]] = None):
+        """`batch_slot_of(times) -> slots` maps report times to aggregate slots (Janus's
+        Q::to_batch_identifier, aggregator.rs:1614-1619); None = one slot."""
+        self.vdaf = vdaf
+        self.task_id = bytes(task_id)
+        self.task_keys = list(task_keys)
+        self.global_keys = list(global_keys)
+        self.query_type = query_type
+        self.hpke_threads = hpke_threads
+        self.batch_slot_of = batch_slot_of
+        self._state = None
+        self._cap = 0
+
+    def open(self, req_bytes: bytes) -> _Opened:
+        """Steps 1-3 (host only)."""
+        s = self.vdaf.sizes
+        req = C.decode_agg_init_req(req_bytes, self.query_type)
+        nonces, pub, lps, st = C.gather_prepare_inits(s, req)
+        pts, offs, st = hpke.open_report_shares(self.task_id, req, self.task_keys,
+                                                self.global_keys, st, self.hpke_threads)
+        hin, st = C.decode_plaintext_input_shares_raw(s, pts, offs, 1, st)
+        slots = None
+        if self.batch_slot_of is not None:
+            slots = np.ascontiguousarray(self.batch_slot_of(req.times()), np.uint32)
+        return _Opened(req.n, nonces, pub, lps, hin, st, slots)
+
+    def prepare(self, o: _Opened, agg: AggregateShares) -> bytes:
+        """Steps 4-5 (GPU + encode)."""
+        if o.n > self._cap:
+            if self._state is not None:
+                self._state.close()
+            self._cap = max(o.n, 2 * self._cap)
+            self._state = self.vdaf.new_state(1, self._cap)
+        msgs, st = self.vdaf.helper_init(self._state, o.nonces, o.public, o.helper_in,
+                                         o.leader_prep, agg=agg, batch_slots=o.slots,
+                                         status=o.status)
+        return C.encode_agg_job_resp(o.nonces, msgs, self.vdaf.sizes.prep_msg, st)
+
+    def handle(self, req_bytes: bytes, agg: AggregateShares) -> bytes:
+        return self.prepare(self.open(req_bytes), agg)
+
+    def handle_jobs(self, reqs: Sequence[bytes], agg: AggregateShares) -> List[bytes]:
+        """Pipelined: host decode + HPKE of job k + 1 overlaps the GPU preparation of job k."""
+        out: List[bytes] = []
+        if not reqs:
+            return out
+        with ThreadPoolExecutor(max_workers=1) as pool:
+            nxt = pool.submit(self.open, reqs[0])
+            for k in range(len(reqs)):
+                cur = nxt.result()
+                if k + 1 < len(reqs):
+                    nxt = pool.submit(self.open, reqs[k + 1])
+                out.append(self.prepare(cur, agg))
+        return out
+
+    def close(self):
+        if self._state is not None:
+            self._state.close()
+            self._state = None
