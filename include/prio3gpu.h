@@ -32,7 +32,8 @@
  * report-major (report r at base + r * <len>).  They may be HOST or DEVICE pointers (detected);
  * device pointers avoid all PCIe traffic.  Errors never fail a whole batch for one report:
  * per-report status bytes mirror DAP `PrepareError` (messages/src/lib.rs:2288-2298):
- *   0 = ok, 5 = VdafPrepError, 8 = InvalidMessage.  A report whose status is non-zero on entry to
+ *   0 = ok, 3 = HpkeUnknownConfigId, 4 = HpkeDecryptError (HPKE stage), 5 = VdafPrepError,
+ *   8 = InvalidMessage.  A report whose status is non-zero on entry to
  * a later stage is skipped by that stage (its outputs are left as zeros).
  * Return codes: 0 = ok, < 0 = API error (bad argument, HIP failure).
  *
