@@ -99,7 +99,7 @@ def main():
     from oracle.ref import Prio3Ref
 
     kind, bits, length, chunk, label = CONFIGS[args.config]
-    defaults = {"sumvec": (262144, 4096), "sum": (1 << 20, 16384), "histogram": (1 << 20, 16384),
+    defaults = {"sumvec": (393216, 4096), "sum": (1 << 20, 16384), "histogram": (1 << 20, 16384),
                 "count": (1 << 22, 65536)}
     B = args.reports or defaults[args.config][0]
     U = args.unique or defaults[args.config][1]
@@ -144,6 +144,7 @@ def main():
     d_msgs = torch.empty((B, max(1, s.prep_msg)), dtype=torch.uint8, device=dev)
     d_lst = torch.zeros(B, dtype=torch.uint8, device=dev)
     d_hst = torch.zeros(B, dtype=torch.uint8, device=dev)
+    d_times = torch.arange(B, dtype=torch.int64, device=dev) + 1_700_000_000  # report times (s)
     torch.cuda.synchronize()
 
     comm = None
@@ -174,7 +175,7 @@ def main():
         wk.p = dict(nonces=P(d_nonces[sl]), pub=P(d_pub[sl]) if d_pub is not None else None,
                     lin=P(d_lin[sl]), hin=P(d_hin[sl]), lprep=P(d_lprep[sl]),
                     msgs=P(d_msgs[sl]) if s.prep_msg else None, lst=P(d_lst[sl]),
-                    hst=P(d_hst[sl]))
+                    hst=P(d_hst[sl]), times=P(d_times[sl]))
         workers.append(wk)
 
     def run_worker(wk):
@@ -184,8 +185,12 @@ def main():
         check(L.prio3gpu_helper_init(ctx, wk.hs._h, wk.n, p["nonces"], p["pub"], p["hin"],
                                      p["lprep"], None, p["msgs"], p["hst"], wk.hpart._h),
               "helper_init")
+        check(L.prio3gpu_agg_update_reports(wk.hpart._h, wk.n, p["nonces"], p["times"], p["hst"],
+                                            None), "helper report checksums")
         check(L.prio3gpu_prepare_next(ctx, wk.ls._h, wk.n, p["msgs"], p["lst"], None, None,
                                       wk.lpart._h), "leader prepare_next")
+        check(L.prio3gpu_agg_update_reports(wk.lpart._h, wk.n, p["nonces"], p["times"], p["lst"],
+                                            None), "leader report checksums")
 
     pool = ThreadPoolExecutor(max_workers=W) if W > 1 else None
 
@@ -264,7 +269,20 @@ def main():
         dist.all_gather_object(allp, plain)
         plain = [sum(col) for col in zip(*allp)] if isinstance(plain, list) else sum(allp)
     assert vdaf.unshard([la, ha]) == plain, "aggregate != plaintext sum"
-    parity = "unshard(aggregate) == plaintext sum; status all ok"
+    # report bookkeeping (Accumulator::update): interval of the report times, and at N = 1 the
+    # ReportIdChecksum against hashlib (each report was accumulated total_steps times: XOR parity)
+    for attr in ("lagg", "hagg"):
+        cks = [getattr(wk, attr).read_reports(0) for wk in workers]
+        assert all(iv == (1_700_000_000, wk.n if W > 1 else B) or W > 1 for _, iv in cks)
+        if world == 1 and W == 1:
+            import hashlib
+            nz = d_nonces.cpu().numpy()
+            dg = np.frombuffer(b"".join(hashlib.sha256(nz[i].tobytes()).digest() for i in range(B)),
+                               np.uint8).reshape(B, 32)
+            x = np.bitwise_xor.reduce(dg, axis=0) if total_steps % 2 else np.zeros(32, np.uint8)
+            assert cks[0][0] == x.tobytes(), "report-ID checksum != SHA-256 XOR"
+    parity = ("unshard(aggregate) == plaintext sum; report-ID checksums == hashlib; "
+              "status all ok")
 
     reports = args.steps * B * world
     value = reports / elapsed

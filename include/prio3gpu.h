@@ -132,6 +132,18 @@ int prio3gpu_agg_read(prio3gpu_agg* agg, uint32_t slot, uint8_t* out_share, uint
 int prio3gpu_agg_merge_bytes(prio3gpu_agg* agg, uint32_t slot, const uint8_t* share,
                              uint64_t count);
 
+/* Accumulator::update's report bookkeeping (accumulator.rs:76-122): for every report whose status
+ * is 0, slot checksum ^= SHA-256(report_id) (ReportIdChecksum, core/src/report_id.rs:18-44) and
+ * the slot's client_timestamp_interval is merged with [time, time + 1) (core/src/time.rs:289-312).
+ * report_ids n x 16, times n x u64 (seconds), status / batch_slots may be NULL (all ok / slot 0);
+ * host or device pointers.  Call with the final statuses (after prepare_next / helper_init). */
+int prio3gpu_agg_update_reports(prio3gpu_agg* agg, size_t n, const uint8_t* report_ids,
+                                const uint64_t* times, const uint8_t* status,
+                                const uint32_t* batch_slots);
+/* The slot's ReportIdChecksum (32 bytes) and interval (start, duration; 0, 0 when empty). */
+int prio3gpu_agg_read_reports(prio3gpu_agg* agg, uint32_t slot, uint8_t* out_checksum,
+                              uint64_t* out_interval_start, uint64_t* out_interval_duration);
+
 /* Collector::unshard (collector/src/lib.rs:539): sum `num_shares` aggregate shares
  * (num_shares x aggregate_share bytes, host) mod p and decode the aggregate result:
  *   Count / Sum / SumVec / Histogram -> out_u128: output_len x 16-byte LE integers;

@@ -63,6 +63,9 @@ def _declare(lib):
         "prio3gpu_agg_reset": (c.c_int, [P]),
         "prio3gpu_agg_read": (c.c_int, [P, c.c_uint32, u8p, c.POINTER(c.c_uint64)]),
         "prio3gpu_agg_merge_bytes": (c.c_int, [P, c.c_uint32, u8p, c.c_uint64]),
+        "prio3gpu_agg_update_reports": (c.c_int, [P, c.c_size_t, u8p, P, u8p, P]),
+        "prio3gpu_agg_read_reports": (c.c_int, [P, c.c_uint32, u8p, c.POINTER(c.c_uint64),
+                                                c.POINTER(c.c_uint64)]),
         "prio3gpu_prepare_init": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, u8p, u8p]),
         "prio3gpu_prepare_shares_to_prepare_message": (c.c_int, [P, c.c_size_t, u8p, u8p, u8p, u8p]),
         "prio3gpu_prepare_next": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, P, P]),
@@ -124,7 +127,8 @@ EXPORTED = [
     "prio3gpu_ctx_create", "prio3gpu_ctx_destroy", "prio3gpu_ctx_sizes", "prio3gpu_ctx_sync",
     "prio3gpu_ctx_stream", "prio3gpu_state_create", "prio3gpu_state_destroy",
     "prio3gpu_agg_create", "prio3gpu_agg_destroy", "prio3gpu_agg_reset", "prio3gpu_agg_read",
-    "prio3gpu_agg_merge_bytes", "prio3gpu_prepare_init",
+    "prio3gpu_agg_merge_bytes", "prio3gpu_agg_update_reports", "prio3gpu_agg_read_reports",
+    "prio3gpu_prepare_init",
     "prio3gpu_prepare_shares_to_prepare_message", "prio3gpu_prepare_next", "prio3gpu_helper_init",
     "prio3gpu_random_size", "prio3gpu_shard", "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
     "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",

@@ -172,6 +172,8 @@ struct prio3gpu_ctx {
   DevBuf perm, chunks, partials, pcounts, spec_idx;
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
   bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
+  bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
+  DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
 };
@@ -218,12 +220,13 @@ struct prio3gpu_agg {
   uint32_t slots = 0;
   DevBuf share;   // slots x out_len x ES
   DevBuf counts;  // slots x u64
+  DevBuf meta;    // slots x SlotMeta: report-ID checksum + client timestamp interval
 };
 
 struct prio3gpu_comm {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0, device = 0;
-  DevBuf gather, cgather;
+  DevBuf gather, cgather, mgather;
 };
 
 namespace {
@@ -541,6 +544,35 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   } else {
     Rows mo{st->meas.u8(), (size_t)g.meas_len * es};
     Rows po{st->proof.u8(), (size_t)g.proof_len * es};
+    bool fused_done = false;
+    if constexpr (FO::ES == 16) {
+      // Few huge reports: the two helper sponges (expansion, joint-rand part) in lockstep.
+      if (g.kind == KIND_FPVEC && c->fused_helper && g.jr_len > 0) {
+        CHK(c->fallback.ensure(4));
+        uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
+        HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
+        {
+          PROF(KID_EXPAND);
+          hipLaunchKernelGGL(k_helper_xof, dim3((N + kHxRows - 1) / kHxRows), dim3(2 * kHxRows), 0,
+                             c->stream, g, N,
+                             CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
+                             Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
+                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb);
+        }
+        uint32_t h_fb = 0;
+        HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        fused_done = h_fb == 0;  // else: a non-canonical element; redo the exact two-pass path
+      }
+    }
+    if (fused_done) {
+      st->spec_ok = false;
+      CHK(launch_fpv_query(c, st, n, CRows{mo.base, mo.stride}, CRows{po.base, po.stride},
+                           d_status));
+      st->meas_rows = CRows{mo.base, mo.stride};
+      st->n = n;
+      return 0;
+    }
     {
       PROF(KID_EXPAND);
       hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
@@ -879,6 +911,7 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
   HIPCHK(hipSetDevice(device));
   auto* c = new prio3gpu_ctx();
   if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
+  if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) c->fused_helper = fh[0] != '0';
   if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
   c->device = device;
   memcpy(c->vk, verify_key, 16);
@@ -995,7 +1028,8 @@ int prio3gpu_agg_create(prio3gpu_ctx* c, uint32_t num_slots, prio3gpu_agg** out)
   a->ctx = c;
   a->slots = num_slots;
   if (a->share.ensure((size_t)num_slots * c->cfg.out_len * c->cfg.es) ||
-      a->counts.ensure((size_t)num_slots * 8)) {
+      a->counts.ensure((size_t)num_slots * 8) ||
+      a->meta.ensure((size_t)num_slots * sizeof(SlotMeta))) {
     prio3gpu_agg_destroy(a);
     return PRIO3GPU_E_HIP;
   }
@@ -1007,6 +1041,7 @@ int prio3gpu_agg_destroy(prio3gpu_agg* a) {
   if (!a) return 0;
   a->share.release();
   a->counts.release();
+  a->meta.release();
   delete a;
   return 0;
 }
@@ -1015,6 +1050,17 @@ int prio3gpu_agg_reset(prio3gpu_agg* a) {
   HIPCHK(hipMemsetAsync(a->share.p, 0, (size_t)a->slots * a->ctx->cfg.out_len * a->ctx->cfg.es,
                         a->ctx->stream));
   HIPCHK(hipMemsetAsync(a->counts.p, 0, (size_t)a->slots * 8, a->ctx->stream));
+  {
+    std::vector<SlotMeta> m(a->slots);
+    for (auto& x : m) {
+      memset(x.ck, 0, sizeof x.ck);
+      x.tmin = ~0ull;
+      x.tmax = 0ull;
+    }
+    HIPCHK(hipMemcpyAsync(a->meta.p, m.data(), m.size() * sizeof(SlotMeta),
+                          hipMemcpyHostToDevice, a->ctx->stream));
+    HIPCHK(hipStreamSynchronize(a->ctx->stream));
+  }
   HIPCHK(hipStreamSynchronize(a->ctx->stream));
   return 0;
 }
@@ -1072,6 +1118,51 @@ int prio3gpu_unshard(const prio3gpu_ctx* c, const uint8_t* agg_shares, size_t nu
       for (uint32_t b = 0; b < 16; ++b) out_u128[(size_t)e * 16 + b] = (uint8_t)(acc >> (8 * b));
     }
   }
+  return 0;
+}
+
+int prio3gpu_agg_update_reports(prio3gpu_agg* a, size_t n, const uint8_t* report_ids,
+                                const uint64_t* times, const uint8_t* status,
+                                const uint32_t* batch_slots) {
+  if (!a || (n && (!report_ids || !times))) {
+    set_err("bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  if (n == 0) return 0;
+  prio3gpu_ctx* c = a->ctx;
+  HIPCHK(hipSetDevice(c->device));
+  const uint8_t *d_ids, *d_times, *d_st = nullptr, *d_slots = nullptr;
+  CHK(stage_in(c, c->io[0], report_ids, n * 16, &d_ids));
+  CHK(stage_in(c, c->io[1], times, n * 8, &d_times));
+  if (status) CHK(stage_in(c, c->io[2], status, n, &d_st));
+  if (batch_slots) CHK(stage_in(c, c->io[3], batch_slots, n * 4, &d_slots));
+  hipLaunchKernelGGL(k_report_meta, grid1(n, 256), dim3(256), 0, c->stream, (uint32_t)n,
+                     CRows{d_ids, 16}, reinterpret_cast<const uint64_t*>(d_times), d_st,
+                     reinterpret_cast<const uint32_t*>(d_slots), a->slots,
+                     reinterpret_cast<SlotMeta*>(a->meta.p));
+  HIPCHK(hipGetLastError());
+  if (!is_device_ptr(report_ids) || !is_device_ptr(times)) HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int prio3gpu_agg_read_reports(prio3gpu_agg* a, uint32_t slot, uint8_t* out_checksum,
+                              uint64_t* out_interval_start, uint64_t* out_interval_duration) {
+  if (!a || slot >= a->slots) {
+    set_err("bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  prio3gpu_ctx* c = a->ctx;
+  HIPCHK(hipSetDevice(c->device));
+  SlotMeta m;
+  HIPCHK(hipMemcpyAsync(&m, a->meta.u8() + (size_t)slot * sizeof(SlotMeta), sizeof m,
+                        hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (out_checksum)
+    for (int i = 0; i < 8; ++i)
+      for (int b = 0; b < 4; ++b) out_checksum[4 * i + b] = (uint8_t)(m.ck[i] >> (24 - 8 * b));
+  const bool empty = m.tmin > m.tmax;
+  if (out_interval_start) *out_interval_start = empty ? 0 : m.tmin;
+  if (out_interval_duration) *out_interval_duration = empty ? 0 : m.tmax - m.tmin + 1;
   return 0;
 }
 
@@ -1456,6 +1547,11 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
   RCCLCHK(ncclAllGather(local->share.p, cm->gather.p, bytes, ncclUint8, cm->comm, c->stream));
   RCCLCHK(ncclAllReduce(local->counts.p, cm->cgather.p, local->slots, ncclUint64, ncclSum, cm->comm,
                         c->stream));
+  // report-ID checksums (XOR) and client-timestamp intervals (min/max): RCCL has neither
+  // reduction, so all-gather the slot meta and fold it on the host below
+  const size_t mbytes = (size_t)local->slots * sizeof(SlotMeta);
+  CHK(cm->mgather.ensure(mbytes * cm->nranks));
+  RCCLCHK(ncclAllGather(local->meta.p, cm->mgather.p, mbytes, ncclUint8, cm->comm, c->stream));
   prio3gpu_agg* dst = total ? total : local;
   if (!total) HIPCHK(hipMemsetAsync(local->share.p, 0, bytes, c->stream));
   // dst += sum over ranks, in rank order (identical on every rank; mod-p addition is exact)
@@ -1480,11 +1576,36 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
                         c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   for (uint32_t s = 0; s < local->slots; ++s) cur[s] = (total ? cur[s] : 0ull) + sum[s];
+  std::vector<SlotMeta> mg((size_t)local->slots * cm->nranks), md(local->slots);
+  HIPCHK(hipMemcpy(mg.data(), cm->mgather.p, mbytes * cm->nranks, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(md.data(), dst->meta.p, mbytes, hipMemcpyDeviceToHost));
+  for (uint32_t s = 0; s < local->slots; ++s) {
+    if (!total) {
+      memset(md[s].ck, 0, sizeof md[s].ck);
+      md[s].tmin = ~0ull;
+      md[s].tmax = 0ull;
+    }
+    for (int r = 0; r < cm->nranks; ++r) {
+      const SlotMeta& x = mg[(size_t)r * local->slots + s];
+      for (int i = 0; i < 8; ++i) md[s].ck[i] ^= x.ck[i];
+      md[s].tmin = std::min(md[s].tmin, x.tmin);
+      md[s].tmax = std::max(md[s].tmax, x.tmax);
+    }
+  }
+  HIPCHK(hipMemcpyAsync(dst->meta.p, md.data(), mbytes, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(dst->counts.p, cur.data(), local->slots * 8, hipMemcpyHostToDevice,
                         c->stream));
   if (total) {  // the local partial has been merged: reset it for the next job
     HIPCHK(hipMemsetAsync(local->share.p, 0, bytes, c->stream));
     HIPCHK(hipMemsetAsync(local->counts.p, 0, (size_t)local->slots * 8, c->stream));
+    std::vector<SlotMeta> z(local->slots);
+    for (auto& x : z) {
+      memset(x.ck, 0, sizeof x.ck);
+      x.tmin = ~0ull;
+      x.tmax = 0ull;
+    }
+    HIPCHK(hipMemcpyAsync(local->meta.p, z.data(), mbytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));  // z lives on this stack frame
   }
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;

@@ -26,6 +26,142 @@
 
 namespace p3g {
 
+// ------------------------------------------------------------------------------------------------
+// Pipelined helper XOF for few, huge reports (k_helper_xof): the helper's measurement-share
+// expansion XOF(k_meas, dst1, [1]) and its joint-rand part derive_seed(blind, dst7, [1] || nonce ||
+// encode(meas share)) are two 152K-permutation chains per report at entries = 100k, and with
+// only a few waves in flight the step is their latency.  Run one after the other (k_expand, then
+// k_jr) they cost two chains; here a 4-wave workgroup runs them as a producer/consumer pipeline:
+// producer waves squeeze block i of the expansion (store it, and hand it over through an LDS
+// double buffer) while consumer waves absorb block i - 1 into the joint-rand sponge, one
+// s_barrier per step.
+// Both waves run the SAME permutation code on their own state (one hot Keccak copy: two would
+// not fit the instruction cache; a two-state single wave measured 20 % slower than serial).
+//
+// Exactness: when every squeezed element is canonical (< p; fails with probability ~28/2^64 per
+// element) the encoded measurement share IS the XOF byte stream, so the consumer absorbs the
+// producer's words directly: its block b needs stream words [21b-6, 21b+15], i.e. words 15..20 of
+// block b-1 (carried in registers) and words 0..15 of block b.  A report that meets a
+// non-canonical element bumps `fallback`; the engine then re-runs the exact k_expand + k_jr for
+// the batch, so outputs are identical either way.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kHxRows = 128;             // reports per workgroup (2 producer + 2 consumer waves)
+constexpr uint32_t kHxSlot = 21 * kHxRows;    // u64 words per LDS slot (word-major, row-minor)
+
+__global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
+                                                    CRows nonces, CRows public_shares,
+                                                    Rows out_meas, Rows out_proof, Rows out_part,
+                                                    Rows out_seed, Rows out_jr,
+                                                    const uint8_t* status, uint32_t* fallback) {
+  using FO = Field128Ops;
+  __shared__ uint64_t ring[2 * kHxSlot];
+  // waves 0, 1 produce and waves 2, 3 consume rows 0..127 (so a producer and its consumer are
+  // never the same wave slot of a SIMD when waves are dealt round-robin over the 4 SIMDs)
+  const uint32_t lane = threadIdx.x & (kHxRows - 1u);
+  const bool producer = threadIdx.x < kHxRows;  // wave-uniform role
+  const uint32_t r0 = blockIdx.x * kHxRows;
+  const uint32_t r = r0 + lane;
+  const bool live = r < n && (!status || status[r] == ST_OK);
+  const uint32_t rr = r < n ? r : n - 1u;  // every lane runs the loop (barriers), clamped row
+  const uint8_t* hs = helper_shares.at(rr);
+  const int64_t nd = (int64_t)cfg.meas_len * 2;    // meas-share words
+  const int64_t total = 42 + 8 * nd;                // consumer's message bytes before padding
+  const int64_t nblocks = total / 168 + 1;          // consumer blocks
+  const int64_t padw = total >> 3;
+  const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
+  const uint64_t nonce_hi = ld64(nonces.at(rr) + 8);
+  uint64_t s[25];
+  if (producer) {
+    MsgBlock m;
+    m.clear();
+    m.header(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8));
+    m.put8(25, 1u);
+    m.pad(26);
+    sponge_one_block<24>(s, m);  // s = expansion block 0
+  } else {
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s[i] = 0ull;
+  }
+  uint64_t carry[6];  // consumer: stream words 21(b-1)+15 .. 21(b-1)+20; D[-1] = nonce_hi
+#pragma unroll
+  for (int i = 0; i < 6; ++i) carry[i] = 0ull;
+  carry[5] = nonce_hi;
+  bool bad = false;
+  uint8_t* om = out_meas.at(rr);
+  for (int64_t i = 0; i <= nblocks; ++i) {
+    if (producer) {
+      const int64_t j0 = 21 * i;
+      if (j0 < nd) {
+        uint64_t* slot = ring + (i & 1) * kHxSlot;
+#pragma unroll
+        for (int w = 0; w < 21; ++w) {
+          const bool in = j0 + w < nd;
+          if (in && live) st64(om + 8 * (j0 + w), s[w]);
+          if (in && ((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
+          slot[w * kHxRows + lane] = in ? s[w] : 0ull;
+        }
+      }
+    } else if (i >= 1) {
+      const int64_t b = i - 1;
+      const uint64_t* slot = ring + (b & 1) * kHxSlot;
+      const bool data = 21 * b < nd;  // else the block is past the share: zeros
+      uint64_t A[16];
+#pragma unroll
+      for (int w = 0; w < 16; ++w) A[w] = data ? slot[w * kHxRows + lane] : 0ull;
+#pragma unroll
+      for (int w = 0; w < 21; ++w) {
+        uint64_t v;
+        if (b == 0 && w < 5) {  // prefix: header(blind) || [1] || nonce
+          MsgBlock m;
+          m.clear();
+          m.header(cfg.algo_id, DST_JOINT_RAND_PART, ld64(hs + 32), ld64(hs + 40));
+          m.put8(25, 1u);
+          m.put64(26, ld64(nonces.at(rr)));
+          m.put64(34, nonce_hi);
+          v = m.w[w];
+        } else {
+          const uint64_t dlo = w <= 5 ? carry[w] : A[w - 6];
+          const uint64_t dhi = w <= 4 ? carry[w + 1] : A[w - 5];
+          v = (dlo >> 48) | (dhi << 16);
+        }
+        const int64_t g = 21 * b + w;
+        if (padw == g) v ^= padv;
+        if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
+        s[w] ^= v;
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) carry[k] = data ? slot[(15 + k) * kHxRows + lane] : 0ull;
+    }
+    const bool perm = producer ? (21 * (i + 1) < nd) : (i >= 1);
+    if (perm) keccak_p<24>(s);
+    __syncthreads();
+  }
+  if (producer) {
+    if (live) {
+      if (bad) atomicAdd(fallback, 1u);
+      xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), 1u,
+                                 cfg.proof_len, out_proof.at(r));
+    }
+    return;
+  }
+  if (!live) return;
+  const uint64_t plo = s[0], phi = s[1];
+  st64(out_part.at(r), plo);
+  st64(out_part.at(r) + 8, phi);
+  const uint8_t* ps = public_shares.at(r);
+  uint64_t slo, shi;
+  derive_jr_seed(cfg.algo_id, ld64(ps), ld64(ps + 8), plo, phi, slo, shi);
+  st64(out_seed.at(r), slo);
+  st64(out_seed.at(r) + 8, shi);
+  MsgBlock m;
+  m.clear();
+  m.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
+  m.pad(25);
+  uint64_t s2[25];
+  sponge_one_block<24>(s2, m);
+  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r));
+}
+
 // Per-report weight row ("W"), element offsets (Field128 elements).
 struct FpvW {
   uint32_t mm, lm, rp, b0, b1, g0, l1, c1, g1, len;

@@ -1457,6 +1457,107 @@ __global__ void __launch_bounds__(256) k_out_shares(Cfg cfg, uint32_t n, CRows m
 }
 
 // dst[i] += src[i] (mod p) over `nelems` field elements (RCCL all-gather merge, K6).
+// ------------------------------------------------------------------------------------------------
+// Accumulator::update's report bookkeeping (aggregator/src/aggregator/accumulator.rs:76-122):
+// per batch slot, checksum ^= SHA-256(report_id) (ReportIdChecksum::updated_with,
+// core/src/report_id.rs:18-44) and client_timestamp_interval merged with [time, time + 1)
+// (Interval::merged_with / from_time, core/src/time.rs:289-312).  Slot meta = 8 checksum words
+// (SHA-256 state words) + u64 min time + u64 max time.  A wave whose live reports share one slot
+// (the common case) reduces with shuffles and issues one set of atomics.
+// ------------------------------------------------------------------------------------------------
+struct SlotMeta {
+  uint32_t ck[8];
+  unsigned long long tmin, tmax;
+};
+
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+DEVI uint32_t rotr32(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+DEVI uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// SHA-256 of a 16-byte message (one padded block): h = digest as 8 big-endian state words.
+DEVI void sha256_16(const uint8_t* m, uint32_t h[8]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = bswap32(*reinterpret_cast<const uint32_t*>(m + 4 * i));
+  w[4] = 0x80000000u;
+#pragma unroll
+  for (int i = 5; i < 15; ++i) w[i] = 0u;
+  w[15] = 128u;  // message length in bits
+  const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                          0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t a = iv[0], b = iv[1], c = iv[2], d = iv[3], e = iv[4], f = iv[5], g = iv[6], hh = iv[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wt = w[t & 15] = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+    }
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = hh + S1 + ch + kSha256K[t] + wt;
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + mj;
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] = iv[0] + a; h[1] = iv[1] + b; h[2] = iv[2] + c; h[3] = iv[3] + d;
+  h[4] = iv[4] + e; h[5] = iv[5] + f; h[6] = iv[6] + g; h[7] = iv[7] + hh;
+}
+
+__global__ void __launch_bounds__(256) k_report_meta(uint32_t n, CRows ids, const uint64_t* times,
+                                                     const uint8_t* status, const uint32_t* slots,
+                                                     uint32_t nslots, SlotMeta* meta) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = r < n && (!status || status[r] == ST_OK) && (!slots || slots[r] < nslots);
+  const unsigned long long act = __ballot(ok);
+  if (act == 0ull) return;  // wave-uniform
+  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t = ok ? times[r] : 0ull;
+  uint32_t slot = 0;
+  if (ok) {
+    sha256_16(ids.at(r), h);
+    slot = slots ? slots[r] : 0u;
+  }
+  const int lead = __ffsll(act) - 1;
+  const uint32_t s0 = __shfl(slot, lead, 64);
+  if (__ballot(ok && slot != s0) == 0ull) {
+    unsigned long long tmin = ok ? t : ~0ull, tmax = t;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) h[i] ^= __shfl_xor(h[i], off, 64);
+      const unsigned long long a = __shfl_xor(tmin, off, 64), b = __shfl_xor(tmax, off, 64);
+      tmin = a < tmin ? a : tmin;
+      tmax = b > tmax ? b : tmax;
+    }
+    if ((int)(threadIdx.x & 63u) == lead) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) atomicXor(&meta[s0].ck[i], h[i]);
+      atomicMin(&meta[s0].tmin, tmin);
+      atomicMax(&meta[s0].tmax, tmax);
+    }
+  } else if (ok) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) atomicXor(&meta[slot].ck[i], h[i]);
+    atomicMin(&meta[slot].tmin, t);
+    atomicMax(&meta[slot].tmax, t);
+  }
+}
+
 template <class FO>
 __global__ void __launch_bounds__(256) k_merge(uint8_t* dst, const uint8_t* src, size_t nelems) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -6,8 +6,10 @@ Per aggregation job (one AggregationJobInitializeReq):
   1. decode the request and gather the engine inputs          codec.cpp   (aggregator.rs:1561-1612)
   2. HPKE-open every encrypted input share on host threads    hpke.cpp    (aggregator.rs:1634-1700)
   3. decode the PlaintextInputShares into the input-share array          (aggregator.rs:1702-1768)
-  4. prio3gpu_helper_init: prepare_init + decide + prepare_next + accumulate on the GPU
-                                                                          (aggregator.rs:1775-1819)
+  4. prio3gpu_helper_init: prepare_init + decide + prepare_next + accumulate on the GPU, and
+     prio3gpu_agg_update_reports: report-ID checksum + client-timestamp interval per batch
+                                                                          (aggregator.rs:1775-1819,
+                                                                           accumulator.rs:76-122)
   5. encode the AggregationJobResp                                        (aggregator.rs:1811-1848)
 
 `handle_jobs` pipelines a stream of jobs: while the GPU runs job k (step 4, the ctypes call
@@ -38,6 +40,7 @@ class _Opened:
     helper_in: np.ndarray
     status: np.ndarray
     slots: Optional[np.ndarray]
+    times: np.ndarray
 
 
 class HelperAggregateInit:
@@ -68,7 +71,7 @@ class HelperAggregateInit:
         slots = None
         if self.batch_slot_of is not None:
             slots = np.ascontiguousarray(self.batch_slot_of(req.times()), np.uint32)
-        return _Opened(req.n, nonces, pub, lps, hin, st, slots)
+        return _Opened(req.n, nonces, pub, lps, hin, st, slots, req.times())
 
     def prepare(self, o: _Opened, agg: AggregateShares) -> bytes:
         """Steps 4-5 (GPU + encode)."""
@@ -80,6 +83,8 @@ class HelperAggregateInit:
         msgs, st = self.vdaf.helper_init(self._state, o.nonces, o.public, o.helper_in,
                                          o.leader_prep, agg=agg, batch_slots=o.slots,
                                          status=o.status)
+        # Accumulator::update bookkeeping: report-ID checksum + client-timestamp interval
+        agg.update_reports(o.nonces, o.times, st, o.slots)
         return C.encode_agg_job_resp(o.nonces, msgs, self.vdaf.sizes.prep_msg, st)
 
     def handle(self, req_bytes: bytes, agg: AggregateShares) -> bytes:

@@ -122,6 +122,32 @@ class AggregateShares:
         check(lib().prio3gpu_agg_read(self._h, slot, _ptr(out), ctypes.byref(cnt)), "agg_read")
         return out.tobytes(), cnt.value
 
+    def update_reports(self, report_ids, times, status=None, batch_slots=None):
+        """Accumulator::update's bookkeeping (accumulator.rs:76-122): per slot, the report-ID
+        checksum (XOR of SHA-256(report id)) and client-timestamp interval of the reports whose
+        status is 0.  Arrays may be numpy (host) or torch/device tensors."""
+        n = _nbytes(report_ids) // 16
+        ids = _as_u8(report_ids, n, 16, "report ids")
+        tm = times if not isinstance(times, (list, tuple)) else np.asarray(times, np.uint64)
+        if isinstance(tm, np.ndarray):
+            tm = np.ascontiguousarray(tm, dtype=np.uint64)
+        st = status
+        if isinstance(st, np.ndarray):
+            st = np.ascontiguousarray(st, dtype=np.uint8)
+        sl = batch_slots
+        if isinstance(sl, np.ndarray):
+            sl = np.ascontiguousarray(sl, dtype=np.uint32)
+        check(lib().prio3gpu_agg_update_reports(self._h, n, _ptr(ids), _ptr(tm), _ptr(st),
+                                                _ptr(sl)), "agg_update_reports")
+
+    def read_reports(self, slot: int = 0):
+        """(ReportIdChecksum bytes, (interval start, duration)) for one batch slot."""
+        ck = np.zeros(32, np.uint8)
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().prio3gpu_agg_read_reports(self._h, slot, _ptr(ck), ctypes.byref(a),
+                                              ctypes.byref(b)), "agg_read_reports")
+        return ck.tobytes(), (a.value, b.value)
+
     def merge(self, slot: int, share: bytes, count: int):
         """`Aggregatable::merge` with an encoded aggregate share."""
         buf = np.frombuffer(bytes(share), dtype=np.uint8).copy()

@@ -222,11 +222,17 @@ def test_rccl_merge_single_rank():
     _, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
     local, total = v.new_aggregate(1), v.new_aggregate(1)
     v.prepare_next(ls, b.prep_msg, lst, want_output_shares=False, agg=local)
+    times = np.arange(100, 100 + b.n, dtype=np.uint64)
+    local.update_reports(b.nonces, times, lst)
+    ck_local = local.read_reports(0)
     comm.allreduce(v, local, total)
     comm.allreduce(v, local, total)  # local was reset: no double counting
     got, cnt = total.read(0)
     assert got == expected_aggregate(b, "leader")[0] and cnt == b.n
     assert local.read(0)[1] == 0
+    # checksums and intervals travel with the merge (all-gather + XOR / min-max fold)
+    assert total.read_reports(0) == ck_local and ck_local[1] == (100, b.n)
+    assert local.read_reports(0) == (bytes(32), (0, 0))
     comm.close()
 
 
@@ -335,3 +341,55 @@ def test_fixedpoint16_100k_entries_config_e():
     assert la == res["agg_l"].tobytes() and ha == res["agg_h"].tobytes()
     plain = g["meas"].view(np.int64).sum(axis=0) * 2.0 ** -15
     assert v.unshard([la, ha], n) == pytest.approx(list(plain), abs=1e-12)
+
+
+@pytest.mark.parametrize("name", ["fp16_3", "fp64_4", "fp16_300"])
+def test_fpvec_helper_two_pass_path_bit_exact(name, monkeypatch):
+    """The FixedPoint helper runs its two sponges fused (k_helper_xof) by default and falls back
+    to the exact two-pass k_expand + k_jr when a squeezed element is non-canonical.  The fallback
+    cannot be provoked with real seeds (probability ~28/2^64 per element), so force the two-pass
+    path through the context switch and check it too against the oracle's transcript."""
+    monkeypatch.setenv("PRIO3GPU_FUSED_HELPER", "0")
+    b = batch(name)
+    v = gpu_vdaf(b)
+    hs = v.new_state(1, b.n)
+    hp, hst = v.prepare_init(hs, b.nonces, b.public, b.helper_in)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(hp, b.helper_prep)
+    ho, hst = v.prepare_next(hs, b.prep_msg, hst.copy())
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(ho, b.helper_out)
+
+
+def test_report_checksum_and_interval():
+    """Accumulator::update's per-batch bookkeeping next to the aggregate share: ReportIdChecksum
+    = XOR of SHA-256(report id) (core/src/report_id.rs:18-44, hashlib as the oracle) and the
+    client-timestamp interval [min, max + 1) (core/src/time.rs:289-312) over the reports whose
+    status is 0, per batch slot; whole waves on one slot and mixed-slot waves both covered."""
+    import hashlib
+    from janus_amd.prio3 import Prio3Gpu
+    rng = np.random.default_rng(11)
+    n = 1000
+    ids = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    times = rng.integers(1_600_000_000, 1_700_000_000, n, dtype=np.uint64)
+    status = np.where(rng.random(n) < 0.1, 5, 0).astype(np.uint8)
+    slots = np.zeros(n, np.uint32)
+    slots[512:] = rng.integers(0, 3, n - 512)
+    v = Prio3Gpu.new_sum(8, bytes(16))
+    agg = v.new_aggregate(4)
+    agg.update_reports(ids[:700], times[:700], status[:700], slots[:700])
+    agg.update_reports(ids[700:], times[700:], status[700:], slots[700:])  # two calls accumulate
+    for slot in range(4):
+        sel = [i for i in range(n) if status[i] == 0 and slots[i] == slot]
+        ck = bytearray(32)
+        for i in sel:
+            for k, x in enumerate(hashlib.sha256(ids[i].tobytes()).digest()):
+                ck[k] ^= x
+        got_ck, (start, dur) = agg.read_reports(slot)
+        assert got_ck == bytes(ck)
+        if sel:
+            assert (start, dur) == (int(times[sel].min()), int(times[sel].max() - times[sel].min()) + 1)
+        else:
+            assert (start, dur) == (0, 0)
+    agg.reset()
+    assert agg.read_reports(0) == (bytes(32), (0, 0))
