@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--workers", type=int, default=1,
@@ -284,6 +285,38 @@ def main():
     parity = ("unshard(aggregate) == plaintext sum; report-ID checksums == hashlib; "
               "status all ok")
 
+    # ---- helper-only variant (the A1 path alone: helper_init + bookkeeping), SURVEY §8(d) -------
+    helper_only = None
+    if args.helper_only:
+        wk = workers[0]
+        p = wk.p
+        hagg2 = wk.v.new_aggregate(1)
+
+        def hstep():
+            d_hst.zero_()
+            check(L.prio3gpu_helper_init(wk.v._ctx, wk.hs._h, wk.n, p["nonces"], p["pub"],
+                                         p["hin"], p["lprep"], None, p["msgs"], p["hst"],
+                                         hagg2._h), "helper_init")
+            check(L.prio3gpu_agg_update_reports(hagg2._h, wk.n, p["nonces"], p["times"], p["hst"],
+                                                None), "helper report checksums")
+        hstep()
+        barrier()
+        th0 = time.perf_counter()
+        for _ in range(args.steps):
+            hstep()
+        barrier()
+        h_el = time.perf_counter() - th0
+        if dist is not None:
+            t = torch.tensor([h_el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            h_el = float(t.item())
+        assert int(d_hst.max().item()) == 0 and hagg2.read(0)[1] == (args.steps + 1) * wk.n
+        helper_only = {"value": round(args.steps * wk.n * world / h_el, 2), "unit": "reports/s",
+                       "ms_per_step": round(h_el / args.steps * 1e3, 3),
+                       "what": "helper aggregate-init alone (prepare_init + decide + prepare_next "
+                               "+ accumulate + report checksums), leader prep shares precomputed"}
+        hagg2.close()
+
     reports = args.steps * B * world
     value = reports / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -410,6 +443,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "hpke_open": hpke_rep,
+        "helper_only": helper_only,
         "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
         "parity": parity,
         "gen_seconds": round(gen_s, 1),

@@ -221,6 +221,7 @@ struct prio3gpu_agg {
   DevBuf share;   // slots x out_len x ES
   DevBuf counts;  // slots x u64
   DevBuf meta;    // slots x SlotMeta: report-ID checksum + client timestamp interval
+  DevBuf wmeta;   // per-wave partials of k_report_meta
 };
 
 struct prio3gpu_comm {
@@ -1042,6 +1043,7 @@ int prio3gpu_agg_destroy(prio3gpu_agg* a) {
   a->share.release();
   a->counts.release();
   a->meta.release();
+  a->wmeta.release();
   delete a;
   return 0;
 }
@@ -1136,9 +1138,15 @@ int prio3gpu_agg_update_reports(prio3gpu_agg* a, size_t n, const uint8_t* report
   CHK(stage_in(c, c->io[1], times, n * 8, &d_times));
   if (status) CHK(stage_in(c, c->io[2], status, n, &d_st));
   if (batch_slots) CHK(stage_in(c, c->io[3], batch_slots, n * 4, &d_slots));
+  const uint32_t nwaves = (uint32_t)((n + 255) / 256 * 4);
+  CHK(a->wmeta.ensure((size_t)nwaves * sizeof(WaveMeta)));
   hipLaunchKernelGGL(k_report_meta, grid1(n, 256), dim3(256), 0, c->stream, (uint32_t)n,
                      CRows{d_ids, 16}, reinterpret_cast<const uint64_t*>(d_times), d_st,
                      reinterpret_cast<const uint32_t*>(d_slots), a->slots,
+                     reinterpret_cast<SlotMeta*>(a->meta.p),
+                     reinterpret_cast<WaveMeta*>(a->wmeta.p));
+  hipLaunchKernelGGL(k_report_meta_fold, dim3(a->slots), dim3(256), 0, c->stream, nwaves,
+                     reinterpret_cast<const WaveMeta*>(a->wmeta.p),
                      reinterpret_cast<SlotMeta*>(a->meta.p));
   HIPCHK(hipGetLastError());
   if (!is_device_ptr(report_ids) || !is_device_ptr(times)) HIPCHK(hipStreamSynchronize(c->stream));

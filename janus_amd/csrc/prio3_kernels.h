@@ -1518,13 +1518,23 @@ DEVI void sha256_16(const uint8_t* m, uint32_t h[8]) {
   h[4] = iv[4] + e; h[5] = iv[5] + f; h[6] = iv[6] + g; h[7] = iv[7] + hh;
 }
 
+struct WaveMeta {
+  SlotMeta m;
+  uint32_t slot;  // 0xFFFFFFFF: no partial (empty or mixed-slot wave)
+  uint32_t pad[3];
+};
+
 __global__ void __launch_bounds__(256) k_report_meta(uint32_t n, CRows ids, const uint64_t* times,
                                                      const uint8_t* status, const uint32_t* slots,
-                                                     uint32_t nslots, SlotMeta* meta) {
+                                                     uint32_t nslots, SlotMeta* meta,
+                                                     WaveMeta* partial) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const bool ok = r < n && (!status || status[r] == ST_OK) && (!slots || slots[r] < nslots);
   const unsigned long long act = __ballot(ok);
-  if (act == 0ull) return;  // wave-uniform
+  if (act == 0ull) {  // wave-uniform
+    if ((threadIdx.x & 63u) == 0u) partial[r >> 6].slot = 0xFFFFFFFFu;
+    return;
+  }
   uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t = ok ? times[r] : 0ull;
   uint32_t slot = 0;
@@ -1534,6 +1544,7 @@ __global__ void __launch_bounds__(256) k_report_meta(uint32_t n, CRows ids, cons
   }
   const int lead = __ffsll(act) - 1;
   const uint32_t s0 = __shfl(slot, lead, 64);
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (__ballot(ok && slot != s0) == 0ull) {
     unsigned long long tmin = ok ? t : ~0ull, tmax = t;
 #pragma unroll
@@ -1544,17 +1555,54 @@ __global__ void __launch_bounds__(256) k_report_meta(uint32_t n, CRows ids, cons
       tmin = a < tmin ? a : tmin;
       tmax = b > tmax ? b : tmax;
     }
+    // one partial per wave; k_report_meta_fold folds them per slot (atomics on one slot's
+    // words from every wave would serialise in L2)
     if ((int)(threadIdx.x & 63u) == lead) {
+      WaveMeta& pw = partial[wave];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) atomicXor(&meta[s0].ck[i], h[i]);
-      atomicMin(&meta[s0].tmin, tmin);
-      atomicMax(&meta[s0].tmax, tmax);
+      for (int i = 0; i < 8; ++i) pw.m.ck[i] = h[i];
+      pw.m.tmin = tmin;
+      pw.m.tmax = tmax;
+      pw.slot = s0;
     }
-  } else if (ok) {
+    return;
+  }
+  if ((threadIdx.x & 63u) == 0u) partial[wave].slot = 0xFFFFFFFFu;  // mixed slots: direct atomics
+  if (ok) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) atomicXor(&meta[slot].ck[i], h[i]);
     atomicMin(&meta[slot].tmin, t);
     atomicMax(&meta[slot].tmax, t);
+  }
+}
+
+// Fold the per-wave partials of k_report_meta: block per slot, one set of atomics per slot.
+__global__ void __launch_bounds__(256) k_report_meta_fold(uint32_t nwaves, const WaveMeta* partial,
+                                                          SlotMeta* meta) {
+  const uint32_t slot = blockIdx.x;
+  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tmin = ~0ull, tmax = 0ull;
+  for (uint32_t w = threadIdx.x; w < nwaves; w += blockDim.x) {
+    const WaveMeta& p = partial[w];
+    if (p.slot != slot) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] ^= p.m.ck[i];
+    tmin = p.m.tmin < tmin ? p.m.tmin : tmin;
+    tmax = p.m.tmax > tmax ? p.m.tmax : tmax;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] ^= __shfl_xor(h[i], off, 64);
+    const unsigned long long a = __shfl_xor(tmin, off, 64), b = __shfl_xor(tmax, off, 64);
+    tmin = a < tmin ? a : tmin;
+    tmax = b > tmax ? b : tmax;
+  }
+  if ((threadIdx.x & 63u) == 0u && tmin <= tmax) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) atomicXor(&meta[slot].ck[i], h[i]);
+    atomicMin(&meta[slot].tmin, tmin);
+    atomicMax(&meta[slot].tmax, tmax);
   }
 }
 
