@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="leader and helper on separate contexts/streams, prepare_init concurrent")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -142,6 +144,8 @@ def main():
     if s.public_share:
         assert np.array_equal(d_pub[:k].cpu().numpy(), chk["public"]), "GPU shard != C shard"
     d_lprep = torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
+    d_hprep = (torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev) if args.overlap
+               else None)
     d_msgs = torch.empty((B, max(1, s.prep_msg)), dtype=torch.uint8, device=dev)
     d_lst = torch.zeros(B, dtype=torch.uint8, device=dev)
     d_hst = torch.zeros(B, dtype=torch.uint8, device=dev)
@@ -168,18 +172,49 @@ def main():
         wk = Worker()
         wk.v, lo, hi = vdafs[w], bounds[w], bounds[w + 1]
         wk.n = hi - lo
-        wk.ls, wk.hs = wk.v.new_state(0, wk.n), wk.v.new_state(1, wk.n)
-        wk.lagg, wk.hagg = wk.v.new_aggregate(1), wk.v.new_aggregate(1)
-        wk.lpart, wk.hpart = ((wk.v.new_aggregate(1), wk.v.new_aggregate(1)) if world > 1
+        # --overlap: the helper gets its own context (HIP stream), so its prepare_init runs
+        # concurrently with the leader's, like two aggregator processes sharing the GPU
+        wk.hv = (Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk,
+                          device=local_rank) if args.overlap else wk.v)
+        wk.ls, wk.hs = wk.v.new_state(0, wk.n), wk.hv.new_state(1, wk.n)
+        wk.lagg, wk.hagg = wk.v.new_aggregate(1), wk.hv.new_aggregate(1)
+        wk.lpart, wk.hpart = ((wk.v.new_aggregate(1), wk.hv.new_aggregate(1)) if world > 1
                               else (wk.lagg, wk.hagg))
         sl = slice(lo, hi)
         wk.p = dict(nonces=P(d_nonces[sl]), pub=P(d_pub[sl]) if d_pub is not None else None,
                     lin=P(d_lin[sl]), hin=P(d_hin[sl]), lprep=P(d_lprep[sl]),
                     msgs=P(d_msgs[sl]) if s.prep_msg else None, lst=P(d_lst[sl]),
-                    hst=P(d_hst[sl]), times=P(d_times[sl]))
+                    hst=P(d_hst[sl]), times=P(d_times[sl]),
+                    hprep=P(d_hprep[sl]) if args.overlap else None)
         workers.append(wk)
 
+    hpool = ThreadPoolExecutor(max_workers=W) if args.overlap else None
+
+    def run_worker_overlap(wk):
+        p, ctx, hctx = wk.p, wk.v._ctx, wk.hv._ctx
+        fut = hpool.submit(L.prio3gpu_prepare_init, hctx, wk.hs._h, wk.n, p["nonces"], p["pub"],
+                           p["hin"], p["hprep"], p["hst"])
+        check(L.prio3gpu_prepare_init(ctx, wk.ls._h, wk.n, p["nonces"], p["pub"], p["lin"],
+                                      p["lprep"], p["lst"]), "leader prepare_init")
+        check(fut.result(), "helper prepare_init")
+        check(L.prio3gpu_prepare_shares_to_prepare_message(hctx, wk.n, p["lprep"], p["hprep"],
+                                                           p["msgs"], p["hst"]), "helper decide")
+
+        def helper_next():
+            check(L.prio3gpu_prepare_next(hctx, wk.hs._h, wk.n, p["msgs"], p["hst"], None, None,
+                                          wk.hpart._h), "helper prepare_next")
+            return L.prio3gpu_agg_update_reports(wk.hpart._h, wk.n, p["nonces"], p["times"],
+                                                 p["hst"], None)
+        fut = hpool.submit(helper_next)
+        check(L.prio3gpu_prepare_next(ctx, wk.ls._h, wk.n, p["msgs"], p["lst"], None, None,
+                                      wk.lpart._h), "leader prepare_next")
+        check(L.prio3gpu_agg_update_reports(wk.lpart._h, wk.n, p["nonces"], p["times"], p["lst"],
+                                            None), "leader report checksums")
+        check(fut.result(), "helper report checksums")
+
     def run_worker(wk):
+        if args.overlap:
+            return run_worker_overlap(wk)
         p, ctx = wk.p, wk.v._ctx
         check(L.prio3gpu_prepare_init(ctx, wk.ls._h, wk.n, p["nonces"], p["pub"], p["lin"],
                                       p["lprep"], p["lst"]), "leader prepare_init")
@@ -206,13 +241,16 @@ def main():
         if comm is not None:  # flush the per-GPU partials into the totals (RCCL + mod-p add)
             for wk in workers:
                 comm.allreduce(wk.v, wk.lpart, wk.lagg)
-                comm.allreduce(wk.v, wk.hpart, wk.hagg)
+                comm.allreduce(wk.hv, wk.hpart, wk.hagg)
 
     for _ in range(args.warmup):
         step()
+    ctxs = []
     for wk in workers:
-        check(L.prio3gpu_prof_enable(wk.v._ctx, 1), "prof")
-        L.prio3gpu_prof_read(wk.v._ctx, (ctypes.c_double * 16)(), (ctypes.c_uint64 * 16)(), 16)
+        ctxs += [wk.v._ctx] + ([wk.hv._ctx] if wk.hv is not wk.v else [])
+    for cx in ctxs:
+        check(L.prio3gpu_prof_enable(cx, 1), "prof")
+        L.prio3gpu_prof_read(cx, (ctypes.c_double * 16)(), (ctypes.c_uint64 * 16)(), 16)
 
     def barrier():
         torch.cuda.synchronize()
@@ -227,16 +265,16 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kt = {}
-    for wk in workers:
+    for cx in ctxs:
         ms = (ctypes.c_double * 16)()
         nl = (ctypes.c_uint64 * 16)()
-        nk = L.prio3gpu_prof_read(wk.v._ctx, ms, nl, 16)
+        nk = L.prio3gpu_prof_read(cx, ms, nl, 16)
         for i in range(nk):
             if nl[i]:
                 name = L.prio3gpu_prof_kernel_name(i).decode()
                 a, b = kt.get(name, (0.0, 0))
                 kt[name] = (a + ms[i], b + nl[i])
-        check(L.prio3gpu_prof_enable(wk.v._ctx, 0), "prof")
+        check(L.prio3gpu_prof_enable(cx, 0), "prof")
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -290,11 +328,11 @@ def main():
     if args.helper_only:
         wk = workers[0]
         p = wk.p
-        hagg2 = wk.v.new_aggregate(1)
+        hagg2 = wk.hv.new_aggregate(1)
 
         def hstep():
             d_hst.zero_()
-            check(L.prio3gpu_helper_init(wk.v._ctx, wk.hs._h, wk.n, p["nonces"], p["pub"],
+            check(L.prio3gpu_helper_init(wk.hv._ctx, wk.hs._h, wk.n, p["nonces"], p["pub"],
                                          p["hin"], p["lprep"], None, p["msgs"], p["hst"],
                                          hagg2._h), "helper_init")
             check(L.prio3gpu_agg_update_reports(hagg2._h, wk.n, p["nonces"], p["times"], p["hst"],

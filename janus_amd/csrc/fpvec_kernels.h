@@ -93,12 +93,34 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
       const int64_t j0 = 21 * i;
       if (j0 < nd) {
         uint64_t* slot = ring + (i & 1) * kHxSlot;
+        if (j0 + 21 <= nd) {  // whole block: 16-B stores (block i starts 16-B aligned iff i even)
+          if (live) {
+            uint8_t* o = om + 8 * j0;
+            if ((i & 1) == 0) {
 #pragma unroll
-        for (int w = 0; w < 21; ++w) {
-          const bool in = j0 + w < nd;
-          if (in && live) st64(om + 8 * (j0 + w), s[w]);
-          if (in && ((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
-          slot[w * kHxRows + lane] = in ? s[w] : 0ull;
+              for (int w = 0; w < 20; w += 2)
+                *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
+              st64(o + 160, s[20]);
+            } else {
+              st64(o, s[0]);
+#pragma unroll
+              for (int w = 1; w < 21; w += 2)
+                *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
+            }
+          }
+#pragma unroll
+          for (int w = 0; w < 21; ++w) {
+            if (((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
+            slot[w * kHxRows + lane] = s[w];
+          }
+        } else {
+#pragma unroll
+          for (int w = 0; w < 21; ++w) {
+            const bool in = j0 + w < nd;
+            if (in && live) st64(om + 8 * (j0 + w), s[w]);
+            if (in && ((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
+            slot[w * kHxRows + lane] = in ? s[w] : 0ull;
+          }
         }
       }
     } else if (i >= 1) {
