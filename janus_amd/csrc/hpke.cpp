@@ -514,7 +514,11 @@ int prio3gpu_hpke_open_report_shares(const uint8_t* task_id, const prio3gpu_hpke
                                      const prio3gpu_prepare_init_view* views, size_t n,
                                      uint8_t* plaintexts, uint64_t* offsets, uint8_t* status,
                                      int threads) {
-  if (!msg || (n && (!views || !offsets))) return PRIO3GPU_E_ARG;
+  if (n == 0) {
+    if (offsets) offsets[0] = 0;
+    return 0;
+  }
+  if (!msg || !views || !offsets) return PRIO3GPU_E_ARG;
   offsets[0] = 0;
   for (size_t i = 0; i < n; ++i)
     offsets[i + 1] = offsets[i] + (views[i].payload_len >= kTag ? views[i].payload_len - kTag : 0);

@@ -925,8 +925,13 @@ DEVI typename FO::T sel(bool c, const typename FO::T& a, const typename FO::T& b
   return o;
 }
 
+// Occupancy hint for the latency-bound weights kernel (wave-level scans / NTT shuffle chains):
+// more waves per SIMD hide the shuffle + Montgomery latencies.
+#ifndef FLPW_WAVES
+#define FLPW_WAVES __attribute__((amdgpu_waves_per_eu(6)))
+#endif
 template <class FO>
-__global__ void __launch_bounds__(256) k_flp_weights(Cfg cfg, uint32_t n, CRows proof, CRows tq,
+__global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_t n, CRows proof, CRows tq,
                                                      CRows jr, CRows part, Rows out_prep,
                                                      uint8_t* status, Rows wrows) {
   using T = typename FO::T;

@@ -184,3 +184,12 @@ def test_pipelined_helper_driver_with_hpke():
     exp, ecnt = expected_aggregate(b, "helper", mask=st == 0)
     assert got == exp and cnt == ecnt == b.n - 2
     drv.close()
+
+
+def test_open_report_shares_empty_request():
+    empty = C.encode_agg_init_req(C.TIME_INTERVAL, None, b"", np.zeros((0, 16), np.uint8), [],
+                                  np.zeros((0, 32), np.uint8), [], np.zeros((0, 4), np.uint8))
+    req = C.decode_agg_init_req(empty)
+    assert req.n == 0
+    pts, offs, st = H.open_report_shares(bytes(32), req, [H.generate_hpke_config_and_private_key(1)])
+    assert offs.tolist() == [0] and st.size == 0

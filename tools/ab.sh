@@ -7,7 +7,7 @@ O=gpurun_out; mkdir -p $O
 for spec in "$@"; do
   label=${spec%%:*}; envs=${spec#*:}
   echo "== $label ($envs)"
-  env $(echo "$envs" | tr ';' ' ') timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --cpu-baseline 0 > $O/ab_${TAG}_$label.log 2>&1
+  env $(echo "$envs" | tr ';' ' ') timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --cpu-baseline 0 --hpke 0 --helper-only 0 > $O/ab_${TAG}_$label.log 2>&1
   rc=$?
   python3 -c "
 import json,sys
