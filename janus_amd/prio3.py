@@ -45,6 +45,36 @@ def chunk_size(measurement_length: int) -> int:
     return int(math.floor(math.sqrt(measurement_length)))
 
 
+def vdaf_instance_params(instance):
+    """(kind, bits, length, chunk_length) for a Janus VdafInstance in its serde form, as
+    `TaskAggregator::new` constructs the VDAF (aggregator/src/aggregator.rs:797-861):
+    CountVec = SumVec with bits 1 and chunk_size(length); SumVec chunk_size(bits * length);
+    Histogram chunk_size(length); FixedPoint{16,32,64}BitBoundedL2VecSum -> bits 16/32/64.
+    Poplar1 and the test-only Fake VDAFs are not Prio3 and are rejected."""
+    if isinstance(instance, str):
+        name, p = instance, {}
+    elif isinstance(instance, dict) and len(instance) == 1:
+        (name, p), = instance.items()
+        p = p or {}
+    else:
+        raise ValueError(f"not a VdafInstance: {instance!r}")
+    if name == "Prio3Count":
+        return COUNT, 0, 0, 0
+    if name == "Prio3CountVec":
+        return SUMVEC, 1, p["length"], chunk_size(p["length"])
+    if name == "Prio3Sum":
+        return SUM, p["bits"], 0, 0
+    if name == "Prio3SumVec":
+        return SUMVEC, p["bits"], p["length"], chunk_size(p["bits"] * p["length"])
+    if name == "Prio3Histogram":
+        return HISTOGRAM, 0, p["length"], chunk_size(p["length"])
+    fp = {"Prio3FixedPoint16BitBoundedL2VecSum": 16, "Prio3FixedPoint32BitBoundedL2VecSum": 32,
+          "Prio3FixedPoint64BitBoundedL2VecSum": 64}
+    if name in fp:
+        return FPVEC, fp[name], p["length"], 0
+    raise ValueError(f"VdafInstance {name} is not served by the Prio3 engine")
+
+
 def _ptr(a) -> Optional[int]:
     """Raw pointer of a numpy array or torch tensor (host or device)."""
     if a is None:
@@ -185,6 +215,14 @@ class Prio3Gpu:
         self.modulus = FIELD64_MODULUS if s.field_size == 8 else FIELD128_MODULUS
 
     # -- constructors mirroring prio (Janus passes num_aggregators = 2) -------------------------
+    @classmethod
+    def from_vdaf_instance(cls, instance, verify_key, device=0):
+        """`TaskAggregator::new`'s VdafInstance -> VDAF mapping (aggregator.rs:797-861).
+        `instance` is Janus's serde form: "Prio3Count" or {"Prio3SumVec": {"bits": 8,
+        "length": 1000}} (core/src/task.rs:24-59)."""
+        kind, bits, length, chunk = vdaf_instance_params(instance)
+        return cls(kind, verify_key, bits=bits, length=length, chunk_length=chunk, device=device)
+
     @classmethod
     def new_count(cls, verify_key, device=0):
         return cls(COUNT, verify_key, device=device)
