@@ -173,6 +173,7 @@ struct prio3gpu_ctx {
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
   bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
   bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
+  uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
@@ -626,8 +627,8 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   const bool psum = (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM);
   if (psum) {
     dims.cols = g.chunk;
-    if (g.chunk <= 256) {
-      dims.H = 256 / g.chunk;
+    if (g.chunk <= c->wires_slots) {
+      dims.H = c->wires_slots / g.chunk;
       if (dims.H > g.calls) dims.H = g.calls;
       nthr = ((dims.H * g.chunk + 63) / 64) * 64;
     } else {
@@ -913,6 +914,10 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
   auto* c = new prio3gpu_ctx();
   if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
   if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) c->fused_helper = fh[0] != '0';
+  if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
+    const long v = strtol(ws, nullptr, 10);
+    if (v >= 64 && v <= 1024) c->wires_slots = (uint32_t)v;
+  }
   if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
   c->device = device;
   memcpy(c->vk, verify_key, 16);

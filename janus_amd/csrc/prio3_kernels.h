@@ -1082,7 +1082,7 @@ __global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_
 // k = 1+h, 1+h+H, ...; lazy-reduced 256-bit MACs, two measurement loads in flight per thread.
 // ------------------------------------------------------------------------------------------------
 template <class FO>
-__global__ void __launch_bounds__(256) k_flp_wires(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
+__global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
                                                    CRows wrows, CRows jr, Rows out_prep,
                                                    uint8_t* status) {
   using T = typename FO::T;
