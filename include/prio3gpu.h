@@ -336,6 +336,12 @@ int prio3gpu_hpke_seal(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id, const
  * core/src/hpke.rs:204-231); PRIO3GPU_E_HPKE if sk is not a valid private key. */
 int prio3gpu_hpke_public_key(uint16_t kem_id, const uint8_t* sk, size_t sk_len, uint8_t* pk,
                              size_t cap, size_t* pk_len);
+/* out[i] = X25519(sk, points[i]) (RFC 7748 §5; the DH of the DHKEM Decap inside hpke::open,
+ * core/src/hpke.rs:184-200) for n 32-byte points under ONE private key.  simd != 0 runs groups of
+ * eight in the AVX-512 IFMA ladder the batched open uses (PRIO3GPU_E_UNSUPPORTED if the host CPU
+ * lacks IFMA); simd == 0 is the scalar ladder.  Exposed so tests can check one against the other. */
+int prio3gpu_x25519_batch(const uint8_t* sk, const uint8_t* points, size_t n, uint8_t* out,
+                          int simd);
 /* Helper: open the n encrypted input shares of a decoded AggregationJobInitializeReq on
  * `threads` host threads (<= 0: all cores), replacing the per-report hpke::open of
  * aggregator.rs:1634-1700: keypair by config id (task keys first, global keys on decryption

@@ -111,6 +111,7 @@ def _declare(lib):
                                          c.c_size_t, c.POINTER(c.c_size_t)]),
         "prio3gpu_hpke_public_key": (c.c_int, [c.c_uint16, u8p, c.c_size_t, u8p, c.c_size_t,
                                                c.POINTER(c.c_size_t)]),
+        "prio3gpu_x25519_batch": (c.c_int, [u8p, u8p, c.c_size_t, u8p, c.c_int]),
         "prio3gpu_hpke_open_report_shares": (c.c_int, [u8p, P, c.c_size_t, P, c.c_size_t,
                                                        c.c_uint8, c.c_uint8, u8p, P, c.c_size_t,
                                                        u8p, P, u8p, c.c_int]),
@@ -137,7 +138,7 @@ EXPORTED = [
     "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",
     "prio3gpu_encode_agg_init_req", "prio3gpu_decode_agg_job_resp", "prio3gpu_gather_helper_resps",
     "prio3gpu_hpke_open", "prio3gpu_hpke_seal", "prio3gpu_hpke_public_key",
-    "prio3gpu_hpke_open_report_shares",
+    "prio3gpu_hpke_open_report_shares", "prio3gpu_x25519_batch",
 ]
 
 

@@ -23,8 +23,11 @@
 #include <openssl/obj_mac.h>
 #include <openssl/rand.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -346,6 +349,195 @@ void x25519(uint8_t* out, const uint8_t* scalar, const uint8_t* point) {
   fe_store(out, x2);
 }
 
+// ---- 8-way X25519 with AVX-512 IFMA ---------------------------------------------------------
+// The helper opens every report of a job with the SAME private key, so the ladder's swap pattern
+// is common to all reports: eight DH computations run in lock step, one report per 64-bit lane,
+// limb-sliced (Fe8.v[i] = limb i of the eight field elements).  Radix 2^51 with limbs < 2^52 (the
+// IFMA input width): vpmadd52lo/hi give the low / high 52 bits of each 52x52 product; a high
+// half weighs 2^52 = 2 * 2^51, so column k = L_k + 2 H_(k-1) (< 15 * 2^52), columns 5..9 fold
+// with 2^255 = 19 (< 2^61), and one parallel carry brings every limb under 2^51 + 2^15.
+// Dispatched at run time (cpuid); both this container's Xeon and the GPU box's EPYC (Zen 5) have
+// IFMA.  Checked against the scalar ladder and the RFC 9180 vectors (tests/test_hpke.py).
+#define IFMA_FN static inline __attribute__((target("avx512f,avx512ifma"), always_inline))
+struct Fe8 { __m512i v[5]; };
+
+IFMA_FN __m512i mul19(__m512i x) {  // x < 2^58
+  return _mm512_add_epi64(_mm512_add_epi64(_mm512_slli_epi64(x, 4), _mm512_slli_epi64(x, 1)), x);
+}
+
+IFMA_FN void fe8_carry(Fe8& h) {  // limbs < 2^62 -> < 2^51 + (input >> 51)
+  const __m512i m = _mm512_set1_epi64(kM51);
+  __m512i c[5];
+  for (int i = 0; i < 5; ++i) c[i] = _mm512_srli_epi64(h.v[i], 51);
+  h.v[0] = _mm512_add_epi64(_mm512_and_si512(h.v[0], m), mul19(c[4]));
+  for (int i = 1; i < 5; ++i) h.v[i] = _mm512_add_epi64(_mm512_and_si512(h.v[i], m), c[i - 1]);
+}
+
+IFMA_FN void fe8_mul(Fe8& h, const Fe8& f, const Fe8& g) {  // f, g limbs < 2^52
+  const __m512i z = _mm512_setzero_si512();
+  __m512i L[9], H[9];
+  for (int k = 0; k < 9; ++k) L[k] = H[k] = z;
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 5; ++j) {
+      L[i + j] = _mm512_madd52lo_epu64(L[i + j], f.v[i], g.v[j]);
+      H[i + j] = _mm512_madd52hi_epu64(H[i + j], f.v[i], g.v[j]);
+    }
+  __m512i col[10];
+  col[0] = L[0];
+  for (int k = 1; k < 9; ++k) col[k] = _mm512_add_epi64(L[k], _mm512_add_epi64(H[k - 1], H[k - 1]));
+  col[9] = _mm512_add_epi64(H[8], H[8]);
+  for (int k = 0; k < 5; ++k) h.v[k] = _mm512_add_epi64(col[k], mul19(col[k + 5]));
+  fe8_carry(h);
+}
+
+IFMA_FN void fe8_sq(Fe8& h, const Fe8& f) {  // 15 products: cross terms doubled in the columns
+  const __m512i z = _mm512_setzero_si512();
+  __m512i L[9], H[9], LD[9], HD[9];
+  for (int k = 0; k < 9; ++k) L[k] = H[k] = LD[k] = HD[k] = z;
+  for (int i = 0; i < 5; ++i) {
+    L[2 * i] = _mm512_madd52lo_epu64(L[2 * i], f.v[i], f.v[i]);
+    H[2 * i] = _mm512_madd52hi_epu64(H[2 * i], f.v[i], f.v[i]);
+    for (int j = i + 1; j < 5; ++j) {
+      LD[i + j] = _mm512_madd52lo_epu64(LD[i + j], f.v[i], f.v[j]);
+      HD[i + j] = _mm512_madd52hi_epu64(HD[i + j], f.v[i], f.v[j]);
+    }
+  }
+  // column k = L_k + 2 LD_k + 2 (H_(k-1) + 2 HD_(k-1));  LD, HD < 2 * 2^52, so col < 2^56
+  __m512i col[10];
+  for (int k = 0; k < 10; ++k) {
+    __m512i c = k < 9 ? _mm512_add_epi64(L[k], _mm512_slli_epi64(LD[k], 1)) : z;
+    if (k > 0)
+      c = _mm512_add_epi64(
+          c, _mm512_slli_epi64(_mm512_add_epi64(H[k - 1], _mm512_slli_epi64(HD[k - 1], 1)), 1));
+    col[k] = c;
+  }
+  for (int k = 0; k < 5; ++k) h.v[k] = _mm512_add_epi64(col[k], mul19(col[k + 5]));
+  fe8_carry(h);
+}
+
+IFMA_FN void fe8_add(Fe8& h, const Fe8& f, const Fe8& g) {
+  for (int i = 0; i < 5; ++i) h.v[i] = _mm512_add_epi64(f.v[i], g.v[i]);
+  fe8_carry(h);
+}
+
+// f - g + 2p;  g limbs <= 2^52 - 38 (every Fe8 value is a carry output: < 2^51 + 2^15)
+IFMA_FN void fe8_sub(Fe8& h, const Fe8& f, const Fe8& g) {
+  const __m512i b0 = _mm512_set1_epi64(0xFFFFFFFFFFFDAll), b = _mm512_set1_epi64(0xFFFFFFFFFFFFEll);
+  for (int i = 0; i < 5; ++i)
+    h.v[i] = _mm512_sub_epi64(_mm512_add_epi64(f.v[i], i ? b : b0), g.v[i]);
+  fe8_carry(h);
+}
+
+IFMA_FN void fe8_cswap(Fe8& a, Fe8& b, uint64_t swap) {
+  const __m512i m = _mm512_set1_epi64((long long)(0 - swap));
+  for (int i = 0; i < 5; ++i) {
+    const __m512i t = _mm512_and_si512(m, _mm512_xor_si512(a.v[i], b.v[i]));
+    a.v[i] = _mm512_xor_si512(a.v[i], t);
+    b.v[i] = _mm512_xor_si512(b.v[i], t);
+  }
+}
+
+IFMA_FN void fe8_sqn(Fe8& h, const Fe8& f, int n) {
+  fe8_sq(h, f);
+  for (int i = 1; i < n; ++i) fe8_sq(h, h);
+}
+
+__attribute__((target("avx512f,avx512ifma"))) void fe8_invert(Fe8& out, const Fe8& z) {
+  Fe8 z2, z9, z11, z_5_0, z_10_0, z_20_0, z_50_0, z_100_0, t;
+  fe8_sq(z2, z);
+  fe8_sqn(t, z2, 2);
+  fe8_mul(z9, t, z);
+  fe8_mul(z11, z9, z2);
+  fe8_sq(t, z11);
+  fe8_mul(z_5_0, t, z9);
+  fe8_sqn(t, z_5_0, 5);
+  fe8_mul(z_10_0, t, z_5_0);
+  fe8_sqn(t, z_10_0, 10);
+  fe8_mul(z_20_0, t, z_10_0);
+  fe8_sqn(t, z_20_0, 20);
+  fe8_mul(t, t, z_20_0);
+  fe8_sqn(t, t, 10);
+  fe8_mul(z_50_0, t, z_10_0);
+  fe8_sqn(t, z_50_0, 50);
+  fe8_mul(z_100_0, t, z_50_0);
+  fe8_sqn(t, z_100_0, 100);
+  fe8_mul(t, t, z_100_0);
+  fe8_sqn(t, t, 50);
+  fe8_mul(t, t, z_50_0);
+  fe8_sqn(t, t, 5);
+  fe8_mul(out, t, z11);
+}
+
+// out[l] = X25519(scalar, points[l]) for l < 8 (one shared scalar)
+__attribute__((target("avx512f,avx512ifma"))) void x25519_x8(uint8_t out[8][32],
+                                                             const uint8_t* scalar,
+                                                             const uint8_t* const points[8]) {
+  uint8_t k[32];
+  memcpy(k, scalar, 32);
+  k[0] &= 248;
+  k[31] &= 127;
+  k[31] |= 64;
+  alignas(64) uint64_t limbs[5][8];
+  for (int l = 0; l < 8; ++l) {
+    Fe p;
+    fe_load(p, points[l]);
+    for (int i = 0; i < 5; ++i) limbs[i][l] = p.v[i];
+  }
+  Fe8 x1, x2, z2, x3, z3, a121665;
+  const __m512i zero = _mm512_setzero_si512(), one = _mm512_set1_epi64(1);
+  for (int i = 0; i < 5; ++i) {
+    x1.v[i] = _mm512_load_si512(limbs[i]);
+    x2.v[i] = z3.v[i] = i ? zero : one;
+    z2.v[i] = zero;
+    a121665.v[i] = i ? zero : _mm512_set1_epi64(121665);
+  }
+  x3 = x1;
+  uint64_t swap = 0;
+  for (int t = 254; t >= 0; --t) {
+    const uint64_t kt = (k[t >> 3] >> (t & 7)) & 1;
+    swap ^= kt;
+    fe8_cswap(x2, x3, swap);
+    fe8_cswap(z2, z3, swap);
+    swap = kt;
+    Fe8 A, AA, B, BB, E, C, D, DA, CB, t0, t1;
+    fe8_add(A, x2, z2);
+    fe8_sq(AA, A);
+    fe8_sub(B, x2, z2);
+    fe8_sq(BB, B);
+    fe8_sub(E, AA, BB);
+    fe8_add(C, x3, z3);
+    fe8_sub(D, x3, z3);
+    fe8_mul(DA, D, A);
+    fe8_mul(CB, C, B);
+    fe8_add(t0, DA, CB);
+    fe8_sq(x3, t0);
+    fe8_sub(t1, DA, CB);
+    fe8_sq(t1, t1);
+    fe8_mul(z3, x1, t1);
+    fe8_mul(x2, AA, BB);
+    fe8_mul(t0, E, a121665);
+    fe8_add(t0, AA, t0);
+    fe8_mul(z2, E, t0);
+  }
+  fe8_cswap(x2, x3, swap);
+  fe8_cswap(z2, z3, swap);
+  Fe8 r;
+  fe8_invert(r, z2);
+  fe8_mul(x2, x2, r);
+  for (int i = 0; i < 5; ++i) _mm512_store_si512(limbs[i], x2.v[i]);
+  for (int l = 0; l < 8; ++l) {
+    Fe h;
+    for (int i = 0; i < 5; ++i) h.v[i] = limbs[i][l];
+    fe_store(out[l], h);
+  }
+}
+
+bool have_ifma() {
+  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512ifma") &&
+                         !getenv("PRIO3GPU_NO_IFMA");
+  return ok;
+}
+
 bool x25519_dh(const uint8_t* sk, const uint8_t* pk, uint8_t* dh) {
   x25519(dh, sk, pk);
   uint8_t acc = 0;  // RFC 9180 §7.1.4: an all-zero X25519 output is an error
@@ -452,13 +644,24 @@ bool aead(const Suite& s, bool encrypt, const uint8_t* key, const uint8_t* nonce
   return ok;
 }
 
+// dh_pre: the DH value already computed for (skR, enc) by the 8-way ladder, or null.
 int open_one(const Suite& s, const uint8_t* skR, size_t sk_len, const uint8_t* pkR, size_t pk_len,
              const uint8_t* enc, size_t enc_len, const uint8_t* info, size_t ilen,
-             const uint8_t* aad, size_t alen, const uint8_t* ct, size_t ct_len, uint8_t* pt) {
+             const uint8_t* aad, size_t alen, const uint8_t* ct, size_t ct_len, uint8_t* pt,
+             const uint8_t* dh_pre = nullptr) {
   if (sk_len != s.nsk || pk_len != s.npk) return PRIO3GPU_E_ARG;
   if (enc_len != s.nenc || ct_len < kTag) return PRIO3GPU_E_HPKE;
   uint8_t dhv[32], ss[32], key[32], nonce[kNonce];
-  if (!dh(s, skR, enc, dhv) || !kem_shared_secret(s, dhv, enc, pkR, ss) ||
+  bool dh_ok;
+  if (dh_pre) {
+    uint8_t acc = 0;  // RFC 9180 §7.1.4: an all-zero X25519 output is an error
+    for (int i = 0; i < 32; ++i) acc |= dh_pre[i];
+    memcpy(dhv, dh_pre, 32);
+    dh_ok = acc != 0;
+  } else {
+    dh_ok = dh(s, skR, enc, dhv);
+  }
+  if (!dh_ok || !kem_shared_secret(s, dhv, enc, pkR, ss) ||
       !key_schedule(s, ss, info, ilen, key, nonce) ||
       !aead(s, false, key, nonce, aad, alen, ct, ct_len, pt))
     return PRIO3GPU_E_HPKE;
@@ -537,6 +740,26 @@ int prio3gpu_hpke_seal(uint16_t kem_id, uint16_t kdf_id, uint16_t aead_id, const
   return 0;
 }
 
+int prio3gpu_x25519_batch(const uint8_t* sk, const uint8_t* points, size_t n, uint8_t* out,
+                          int simd) {
+  if (n && (!sk || !points || !out)) return PRIO3GPU_E_ARG;
+  if (simd && !have_ifma()) return PRIO3GPU_E_UNSUPPORTED;
+  size_t i = 0;
+  if (simd) {
+    for (; i < n; i += 8) {
+      const uint8_t* pts[8];
+      const size_t m = std::min<size_t>(8, n - i);
+      for (size_t l = 0; l < 8; ++l) pts[l] = points + 32 * (i + (l < m ? l : 0));
+      uint8_t o[8][32];
+      x25519_x8(o, sk, pts);
+      for (size_t l = 0; l < m; ++l) memcpy(out + 32 * (i + l), o[l], 32);
+    }
+    return 0;
+  }
+  for (; i < n; ++i) x25519(out + 32 * i, sk, points + 32 * i);
+  return 0;
+}
+
 int prio3gpu_hpke_public_key(uint16_t kem_id, const uint8_t* sk, size_t sk_len, uint8_t* pk,
                              size_t cap, size_t* pk_len) {
   Suite s;
@@ -574,7 +797,9 @@ int prio3gpu_hpke_open_report_shares(const uint8_t* task_id, const prio3gpu_hpke
       if (ks[k].config_id == id) return &ks[k];
     return static_cast<const prio3gpu_hpke_keypair*>(nullptr);
   };
-  parallel_for(n, threads, [&](size_t i) {
+  // One report: InputShareAad, the first-choice key (with its DH precomputed by the 8-way
+  // ladder when dh_pre is set), then the global key after a decryption failure.
+  auto open_i = [&](size_t i, const uint8_t* dh_pre) {
     if (status[i]) return;
     const prio3gpu_prepare_init_view& v = views[i];
     const prio3gpu_hpke_keypair* tk = find(task_keys, n_task_keys, v.hpke_config_id);
@@ -591,17 +816,57 @@ int prio3gpu_hpke_open_report_shares(const uint8_t* task_id, const prio3gpu_hpke
     aad.add(task_id, 32).add(msg + v.report_id_off, 16).add(tbe, 8).add(plbe, 4);
     aad.add(msg + v.public_share_off, pl);
     uint8_t* out = plaintexts + offsets[i];
-    auto try_open = [&](const prio3gpu_hpke_keypair* kp) -> int {
+    auto try_open = [&](const prio3gpu_hpke_keypair* kp, const uint8_t* pre) -> int {
       Suite s;
       if (!suite_of(kp->kem_id, kp->kdf_id, kp->aead_id, &s)) return PRIO3GPU_E_UNSUPPORTED;
       return open_one(s, kp->private_key, kp->private_key_len, kp->public_key,
                       kp->public_key_len, msg + v.enc_off, v.enc_len, info.v.data(),
                       info.v.size(), aad.v.data(), aad.v.size(), msg + v.payload_off,
-                      v.payload_len, out);
+                      v.payload_len, out, pre);
     };
-    int rc = try_open(tk ? tk : gk);
-    if (rc == PRIO3GPU_E_HPKE && tk && gk) rc = try_open(gk);  // second trial on decrypt failure
+    int rc = try_open(tk ? tk : gk, dh_pre);
+    if (rc == PRIO3GPU_E_HPKE && tk && gk) rc = try_open(gk, nullptr);  // second trial
     if (rc != 0) status[i] = 4;  // PrepareError::HpkeDecryptError
+  };
+  auto primary = [&](size_t i) {
+    const uint8_t id = views[i].hpke_config_id;
+    const prio3gpu_hpke_keypair* tk = find(task_keys, n_task_keys, id);
+    return tk ? tk : find(global_keys, n_global_keys, id);
+  };
+  const bool simd = have_ifma();
+  // Chunks of 8 reports: the X25519 DH of every report whose first-choice key is the chunk's
+  // common X25519 key runs in the 8-way ladder; the rest (P-256, mixed keys, the global-key
+  // retry) take the scalar path inside open_one.
+  parallel_for((n + 7) / 8, threads, [&](size_t ch) {
+    const size_t b = ch * 8, e = std::min(n, b + 8);
+    uint8_t dh8[8][32];
+    bool pre[8] = {};
+    if (simd) {
+      const prio3gpu_hpke_keypair* kp0 = nullptr;
+      const uint8_t* pts[8];
+      int lanes = 0;
+      for (size_t i = b; i < e; ++i) {
+        if (status[i]) continue;
+        const prio3gpu_hpke_keypair* kp = primary(i);
+        if (!kp || kp->kem_id != KEM_X25519 || kp->private_key_len != 32 || views[i].enc_len != 32)
+          continue;
+        if (!kp0) kp0 = kp;
+        if (kp != kp0) continue;
+        pre[i - b] = true;
+        pts[lanes++] = msg + views[i].enc_off;
+      }
+      if (lanes >= 2) {
+        for (int l = lanes; l < 8; ++l) pts[l] = pts[0];
+        uint8_t out[8][32];
+        x25519_x8(out, kp0->private_key, pts);
+        int l = 0;
+        for (size_t i = b; i < e; ++i)
+          if (pre[i - b]) memcpy(dh8[i - b], out[l++], 32);
+      } else {
+        for (bool& p : pre) p = false;
+      }
+    }
+    for (size_t i = b; i < e; ++i) open_i(i, pre[i - b] ? dh8[i - b] : nullptr);
   });
   return 0;
 }

@@ -193,3 +193,65 @@ def test_open_report_shares_empty_request():
     assert req.n == 0
     pts, offs, st = H.open_report_shares(bytes(32), req, [H.generate_hpke_config_and_private_key(1)])
     assert offs.tolist() == [0] and st.size == 0
+
+
+def _x25519_batch(sk: bytes, points: bytes, simd: int) -> bytes:
+    import ctypes
+    from janus_amd._lib import lib
+    n = len(points) // 32
+    out = ctypes.create_string_buffer(32 * max(n, 1))
+    rc = lib().prio3gpu_x25519_batch(sk, points, n, out, simd)
+    if rc == -6:
+        pytest.skip("host CPU has no AVX-512 IFMA")
+    assert rc == 0
+    return out.raw[:32 * n]
+
+
+@pytest.mark.parametrize("n", [1, 3, 8, 13, 64])
+def test_x25519_ifma_ladder_matches_scalar(n):
+    """The 8-way IFMA ladder the batched open uses == the scalar radix-2^51 ladder, including
+    points with bit 255 set and non-canonical u-coordinates (>= p), and ragged groups."""
+    rng = np.random.default_rng(n)
+    sk = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    pts = bytearray(rng.integers(0, 256, 32 * n, dtype=np.uint8).tobytes())
+    pts[31] |= 0x80
+    if n > 1:  # u = p + 3 (non-canonical) and u = 2^255 - 1
+        pts[32:64] = ((1 << 255) - 19 + 3).to_bytes(32, "little")
+    if n > 2:
+        pts[64:96] = b"\xff" * 32
+    assert _x25519_batch(sk, bytes(pts), 1) == _x25519_batch(sk, bytes(pts), 0)
+
+
+def test_x25519_ifma_rfc7748_vectors():
+    # RFC 7748 §5.2 test vectors 1 and 2, both through one 8-way group
+    k1 = bytes.fromhex("a546e36bf0527c9d3b16154b82465edd62144c0ac1fc5a18506a2244ba449ac4")
+    u1 = bytes.fromhex("e6db6867583030db3594c1a424b15f7c726624ec26b3353b10a903a6d0ab1c4c")
+    r1 = "c3da55379de9c6908e94ea4df28d084f32eccf03491c71f754b4075577a28552"
+    k2 = bytes.fromhex("4b66e9d4d1b4673c5ad22691957d6af5c11b6421e0ea01d42ca4169e7918ba0d")
+    u2 = bytes.fromhex("e5210f12786811d3f4b7959d0538ae2c31dbe7106fc03c3efc4cd549c715a493")
+    r2 = "95cbde9476e8907d7aade45cb4b873f88b595a68799fa152e6f8f7647aac7957"
+    assert _x25519_batch(k1, u1 * 3, 1).hex() == r1 * 3
+    assert _x25519_batch(k2, u2 * 9, 1).hex() == r2 * 9
+
+
+def test_open_report_shares_one_key_batch_matches_single_opens():
+    """A batch sealed to one X25519 key (the helper's common case: every chunk of 8 goes through
+    the IFMA ladder, with a ragged tail) opens exactly like per-report hpke::open."""
+    rng = np.random.default_rng(11)
+    n = 37
+    task_id = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    tk = H.generate_hpke_config_and_private_key(4)
+    nonces = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    times = [1_600_000_000 + 7 * i for i in range(n)]
+    public = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    payloads = [bytes(rng.integers(0, 256, 48, dtype=np.uint8)) for _ in range(n)]
+    req = C.decode_agg_init_req(_request(task_id, nonces, times, public, payloads, [tk] * n))
+    v = req.views[20]
+    req.raw[v.payload_off] ^= 1  # one bad tag inside a full SIMD group
+    pts, offs, st = H.open_report_shares(task_id, req, [tk], [], np.zeros(n, np.uint8), threads=3)
+    for i in range(n):
+        if i == 20:
+            assert st[i] == 4
+            continue
+        assert st[i] == 0, i
+        assert pts[int(offs[i]):int(offs[i + 1])].tobytes()[6:] == payloads[i]
