@@ -418,6 +418,19 @@ IFMA_FN void fe8_mul(Fe8& h, const Fe8& f, const Fe8& g) {  // f, g limbs < 2^52
   fe8_carry(h);
 }
 
+IFMA_FN void fe8_mul_small(Fe8& h, const Fe8& f, uint64_t k) {  // k < 2^52: 10 products
+  const __m512i z = _mm512_setzero_si512(), kk = _mm512_set1_epi64((long long)k);
+  __m512i lo[5], hi[5];
+  for (int i = 0; i < 5; ++i) {
+    lo[i] = _mm512_madd52lo_epu64(z, f.v[i], kk);
+    hi[i] = _mm512_madd52hi_epu64(z, f.v[i], kk);
+  }
+  // column i = lo_i + 2 hi_(i-1); column 5 = 2 hi_4 folds into column 0 with x19
+  h.v[0] = _mm512_add_epi64(lo[0], mul19(_mm512_add_epi64(hi[4], hi[4])));
+  for (int i = 1; i < 5; ++i) h.v[i] = _mm512_add_epi64(lo[i], _mm512_add_epi64(hi[i - 1], hi[i - 1]));
+  fe8_carry(h);
+}
+
 IFMA_FN void fe8_sq(Fe8& h, const Fe8& f) {  // 15 products: cross terms doubled in the columns
   const __m512i z = _mm512_setzero_si512();
   __m512i L[9], H[9], LD[9], HD[9];
@@ -511,13 +524,12 @@ __attribute__((target("avx512f,avx512ifma"))) void x25519_x8(uint8_t out[8][32],
     fe_load(p, points[l]);
     for (int i = 0; i < 5; ++i) limbs[i][l] = p.v[i];
   }
-  Fe8 x1, x2, z2, x3, z3, a121665;
+  Fe8 x1, x2, z2, x3, z3;
   const __m512i zero = _mm512_setzero_si512(), one = _mm512_set1_epi64(1);
   for (int i = 0; i < 5; ++i) {
     x1.v[i] = _mm512_load_si512(limbs[i]);
     x2.v[i] = z3.v[i] = i ? zero : one;
     z2.v[i] = zero;
-    a121665.v[i] = i ? zero : _mm512_set1_epi64(121665);
   }
   x3 = x1;
   uint64_t swap = 0;
@@ -543,7 +555,7 @@ __attribute__((target("avx512f,avx512ifma"))) void x25519_x8(uint8_t out[8][32],
     fe8_sq(t1, t1);
     fe8_mul(z3, x1, t1);
     fe8_mul(x2, AA, BB);
-    fe8_mul(t0, E, a121665);
+    fe8_mul_small(t0, E, 121665);
     fe8_add(t0, AA, t0);
     fe8_mul(z2, E, t0);
   }
