@@ -72,7 +72,9 @@ class AggInitReq:
 
 
 def decode_agg_init_req(msg: bytes, query_type: int = TIME_INTERVAL) -> AggInitReq:
-    raw = _u8(msg).copy()
+    # no copy of the (up to hundreds of MB) request: bytes give a read-only view, a bytearray or
+    # ndarray a writable one that aliases the caller's buffer
+    raw = msg if isinstance(msg, np.ndarray) else np.frombuffer(msg, dtype=np.uint8)
     n = ctypes.c_size_t()
     check(lib().prio3gpu_decode_agg_init_req(_p(raw), raw.size, query_type, None, None, None, 0,
                                              ctypes.byref(n)), "decode AggregationJobInitializeReq")
@@ -86,13 +88,20 @@ def decode_agg_init_req(msg: bytes, query_type: int = TIME_INTERVAL) -> AggInitR
                       bid.tobytes() if query_type == FIXED_SIZE else None)
 
 
-def gather_prepare_inits(sizes, req: AggInitReq, status: Optional[np.ndarray] = None):
-    """(nonces, public shares, leader prep shares, status) for prio3gpu_helper_init."""
+def gather_prepare_inits(sizes, req: AggInitReq, status: Optional[np.ndarray] = None,
+                         lps_out: Optional[np.ndarray] = None):
+    """(nonces, public shares, leader prep shares, status) for prio3gpu_helper_init.  `lps_out`:
+    optional (>= n, prep_share) uint8 buffer (e.g. pinned host memory) for the prep shares."""
     n = req.n
     st = np.zeros(n, np.uint8) if status is None else status
     nonces = np.zeros((n, 16), np.uint8)
     pub = np.zeros((n, sizes.public_share), np.uint8)
-    lps = np.zeros((n, sizes.prep_share), np.uint8)
+    if lps_out is not None:
+        assert lps_out.dtype == np.uint8 and lps_out.flags.c_contiguous
+        assert lps_out.shape[0] >= n and lps_out.shape[1] == sizes.prep_share
+        lps = lps_out[:n]
+    else:
+        lps = np.zeros((n, sizes.prep_share), np.uint8)
     check(lib().prio3gpu_gather_prepare_inits(ctypes.byref(sizes), _p(req.raw), req.views, n,
                                               _p(nonces), _p(pub), _p(lps), _p(st)), "gather")
     return nonces, pub, lps, st

@@ -59,12 +59,18 @@ class HelperAggregateInit:
         self.batch_slot_of = batch_slot_of
         self._state = None
         self._cap = 0
+        # two pinned staging buffers for the leader prep shares (the largest per-report input,
+        # 2,896 B for SumVec): job k+1 is gathered into one while job k's is copied to the GPU
+        # from the other; pageable memory would make that copy the slowest step.
+        self._pinned: List[Optional[np.ndarray]] = [None, None]
+        self._pin_keep: List[object] = [None, None]
+        self._next_buf = 0
 
     def open(self, req_bytes: bytes) -> _Opened:
         """Steps 1-3 (host only)."""
         s = self.vdaf.sizes
         req = C.decode_agg_init_req(req_bytes, self.query_type)
-        nonces, pub, lps, st = C.gather_prepare_inits(s, req)
+        nonces, pub, lps, st = C.gather_prepare_inits(s, req, lps_out=self._staging(req.n))
         pts, offs, st = hpke.open_report_shares(self.task_id, req, self.task_keys,
                                                 self.global_keys, st, self.hpke_threads)
         hin, st = C.decode_plaintext_input_shares_raw(s, pts, offs, 1, st)
@@ -72,6 +78,22 @@ class HelperAggregateInit:
         if self.batch_slot_of is not None:
             slots = np.ascontiguousarray(self.batch_slot_of(req.times()), np.uint32)
         return _Opened(req.n, nonces, pub, lps, hin, st, slots, req.times())
+
+    def _staging(self, n: int) -> Optional[np.ndarray]:
+        """Pinned buffer for the next job's leader prep shares (alternating), or None off-GPU."""
+        import torch
+        if n == 0 or not torch.cuda.is_available():
+            return None
+        k = self._next_buf
+        self._next_buf ^= 1
+        buf = self._pinned[k]
+        ps = self.vdaf.sizes.prep_share
+        if buf is None or buf.shape[0] < n:
+            t = torch.empty((max(n, 2 * (0 if buf is None else buf.shape[0])), ps),
+                            dtype=torch.uint8, pin_memory=True)
+            self._pin_keep[k] = t
+            self._pinned[k] = buf = t.numpy()
+        return buf
 
     def prepare(self, o: _Opened, agg: AggregateShares) -> bytes:
         """Steps 4-5 (GPU + encode)."""
@@ -108,3 +130,5 @@ class HelperAggregateInit:
         if self._state is not None:
             self._state.close()
             self._state = None
+        self._pinned = [None, None]
+        self._pin_keep = [None, None]

@@ -111,7 +111,7 @@ def test_open_report_shares_key_selection_and_errors():
     payloads = [bytes(rng.integers(0, 256, 48, dtype=np.uint8)) for _ in range(n)]
     kps = [tk if i % 3 == 0 else gk if i % 3 == 1 else gk_same_id for i in range(n)]
     kps[5] = None  # unknown config id
-    req = C.decode_agg_init_req(_request(task_id, nonces, times, public, payloads, kps))
+    req = C.decode_agg_init_req(bytearray(_request(task_id, nonces, times, public, payloads, kps)))
     # corrupt report 7's payload in place (AEAD tag check fails)
     v = req.views[7]
     req.raw[v.payload_off + 3] ^= 0x40
@@ -245,7 +245,8 @@ def test_open_report_shares_one_key_batch_matches_single_opens():
     times = [1_600_000_000 + 7 * i for i in range(n)]
     public = rng.integers(0, 256, (n, 32), dtype=np.uint8)
     payloads = [bytes(rng.integers(0, 256, 48, dtype=np.uint8)) for _ in range(n)]
-    req = C.decode_agg_init_req(_request(task_id, nonces, times, public, payloads, [tk] * n))
+    req = C.decode_agg_init_req(bytearray(_request(task_id, nonces, times, public, payloads,
+                                                   [tk] * n)))
     v = req.views[20]
     req.raw[v.payload_off] ^= 1  # one bad tag inside a full SIMD group
     pts, offs, st = H.open_report_shares(task_id, req, [tk], [], np.zeros(n, np.uint8), threads=3)
