@@ -650,11 +650,27 @@ bool key_schedule(const Suite& s, const uint8_t* ss, const uint8_t* info, size_t
   const EVP_MD* md = algs().md[s.kdf];
   Bytes sid;
   sid.add("HPKE").u16(s.kem).u16(s.kdf).u16(s.aead);
-  uint8_t psk_id_hash[kMaxHash], info_hash[kMaxHash], secret[kMaxHash];
-  if (!labeled_extract(md, sid, nullptr, 0, "psk_id_hash", nullptr, 0, psk_id_hash) ||
-      !labeled_extract(md, sid, nullptr, 0, "info_hash", info, ilen, info_hash) ||
-      !labeled_extract(md, sid, ss, s.nsecret, "secret", nullptr, 0, secret))
-    return false;
+  // psk_id_hash and info_hash depend only on the suite and info, which a batch of opens shares:
+  // cached per thread (keyed by suite and info bytes).
+  struct Cached {
+    uint16_t kem = 0, kdf = 0, aead = 0;
+    std::vector<uint8_t> info;
+    uint8_t psk_id_hash[kMaxHash], info_hash[kMaxHash];
+  };
+  thread_local Cached cache;
+  if (cache.kem != s.kem || cache.kdf != s.kdf || cache.aead != s.aead ||
+      cache.info.size() != ilen || (ilen && memcmp(cache.info.data(), info, ilen) != 0)) {
+    cache.kem = 0;
+    if (!labeled_extract(md, sid, nullptr, 0, "psk_id_hash", nullptr, 0, cache.psk_id_hash) ||
+        !labeled_extract(md, sid, nullptr, 0, "info_hash", info, ilen, cache.info_hash))
+      return false;
+    cache.info.assign(info, info + ilen);
+    cache.kem = s.kem, cache.kdf = s.kdf, cache.aead = s.aead;
+  }
+  const uint8_t* psk_id_hash = cache.psk_id_hash;
+  const uint8_t* info_hash = cache.info_hash;
+  uint8_t secret[kMaxHash];
+  if (!labeled_extract(md, sid, ss, s.nsecret, "secret", nullptr, 0, secret)) return false;
   Bytes ksc;
   const uint8_t mode = 0;
   ksc.add(&mode, 1).add(psk_id_hash, s.nh).add(info_hash, s.nh);
