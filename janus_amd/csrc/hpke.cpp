@@ -134,8 +134,14 @@ struct Sha2 {
   }
 };
 
-bool hmac(const EVP_MD* md, const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
-          uint8_t* out) {
+struct Seg {
+  const void* p;
+  size_t n;
+};
+
+// HMAC over the concatenation of segs (no intermediate message buffer).
+bool hmac_segs(const EVP_MD* md, const uint8_t* key, size_t klen, const Seg* segs, int nseg,
+               uint8_t* out) {
   const size_t hl = EVP_MD_get_size(md), bs = hl == 32 ? 64 : 128;
   uint8_t k0[128] = {0}, pad[128];
   if (klen > bs) {
@@ -149,7 +155,8 @@ bool hmac(const EVP_MD* md, const uint8_t* key, size_t klen, const uint8_t* msg,
   for (size_t i = 0; i < bs; ++i) pad[i] = k0[i] ^ 0x36;
   Sha2 hi(hl);
   hi.update(pad, bs);
-  hi.update(msg, mlen);
+  for (int k = 0; k < nseg; ++k)
+    if (segs[k].n) hi.update(segs[k].p, segs[k].n);
   hi.final(inner);
   for (size_t i = 0; i < bs; ++i) pad[i] = k0[i] ^ 0x5c;
   Sha2 ho(hl);
@@ -159,29 +166,33 @@ bool hmac(const EVP_MD* md, const uint8_t* key, size_t klen, const uint8_t* msg,
   return true;
 }
 
+bool hmac(const EVP_MD* md, const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen,
+          uint8_t* out) {
+  const Seg seg{msg, mlen};
+  return hmac_segs(md, key, klen, &seg, 1, out);
+}
+
 // LabeledExtract(salt, label, ikm) = HMAC(salt, "HPKE-v1" || suite_id || label || ikm)  (§4)
 bool labeled_extract(const EVP_MD* md, const Bytes& suite_id, const uint8_t* salt, size_t slen,
                      const char* label, const uint8_t* ikm, size_t ilen, uint8_t* prk) {
-  Bytes m;
-  m.add("HPKE-v1").add(suite_id.v.data(), suite_id.v.size()).add(label).add(ikm, ilen);
-  return hmac(md, salt, slen, m.v.data(), m.v.size(), prk);
+  const Seg segs[4] = {{"HPKE-v1", 7}, {suite_id.v.data(), suite_id.v.size()},
+                       {label, strlen(label)}, {ikm, ilen}};
+  return hmac_segs(md, salt, slen, segs, 4, prk);
 }
 
 // LabeledExpand(prk, label, info, L) = HKDF-Expand(prk, I2OSP(L,2) || "HPKE-v1" || suite_id ||
 // label || info, L)
 bool labeled_expand(const EVP_MD* md, const Bytes& suite_id, const uint8_t* prk, size_t plen,
                     const char* label, const uint8_t* info, size_t ilen, size_t L, uint8_t* out) {
-  Bytes li;
-  li.u16(uint16_t(L)).add("HPKE-v1").add(suite_id.v.data(), suite_id.v.size()).add(label);
-  li.add(info, ilen);
   const size_t hl = EVP_MD_get_size(md);
   if (L > 255 * hl) return false;
+  const uint8_t lbe[2] = {uint8_t(L >> 8), uint8_t(L)};
   uint8_t t[kMaxHash];
   size_t tl = 0, done = 0;
   for (uint8_t i = 1; done < L; ++i) {
-    Bytes m;
-    m.add(t, tl).add(li.v.data(), li.v.size()).add(&i, 1);
-    if (!hmac(md, prk, plen, m.v.data(), m.v.size(), t)) return false;
+    const Seg segs[7] = {{t, tl},     {lbe, 2},     {"HPKE-v1", 7}, {suite_id.v.data(), suite_id.v.size()},
+                         {label, strlen(label)}, {info, ilen}, {&i, 1}};
+    if (!hmac_segs(md, prk, plen, segs, 7, t)) return false;
     tl = hl;
     const size_t c = std::min(hl, L - done);
     memcpy(out + done, t, c);
