@@ -68,7 +68,12 @@ class AggInitReq:
                  self.field(i, "payload_off", "payload_len")) for i in range(self.n)]
 
     def times(self) -> np.ndarray:
-        return np.array([self.views[i].time for i in range(self.n)], dtype=np.uint64)
+        if self.n == 0:
+            return np.zeros(0, np.uint64)
+        # the views' `time` column read straight from the ctypes array (no per-report loop)
+        sz, off = ctypes.sizeof(PrepareInitView), PrepareInitView.time.offset
+        rows = np.frombuffer(self.views, dtype=np.uint8)[:self.n * sz].reshape(self.n, sz)
+        return np.ascontiguousarray(rows[:, off:off + 8]).view("<u8").reshape(self.n)
 
 
 def decode_agg_init_req(msg: bytes, query_type: int = TIME_INTERVAL) -> AggInitReq:
