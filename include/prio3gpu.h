@@ -80,7 +80,11 @@ enum prio3gpu_err {
   PRIO3GPU_E_RCCL = -3,
   PRIO3GPU_E_CAPACITY = -4,
   PRIO3GPU_E_HPKE = -5,        /* HPKE open/seal failed (bad key, tag mismatch) */
-  PRIO3GPU_E_UNSUPPORTED = -6  /* HPKE suite not supported */
+  PRIO3GPU_E_UNSUPPORTED = -6, /* HPKE suite not supported */
+  /* The whole request is invalid (DAP "invalidMessage" for the request, not one report):
+   * duplicate report IDs (aggregator.rs:1588-1598), an aggregation parameter that is not
+   * Prio3's empty `()` (aggregator.rs:1605). */
+  PRIO3GPU_E_INVALID_MESSAGE = -7
 };
 
 typedef struct prio3gpu_ctx prio3gpu_ctx;
@@ -258,18 +262,35 @@ typedef struct prio3gpu_prepare_resp_view {
 
 /* AggregationJobInitializeReq -> one view per PrepareInit.  views == NULL counts only.
  * out_agg_param (may be NULL) = {offset, length}; out_batch_id (FixedSize, may be NULL) 32 bytes.
- * A malformed request is an API error (Janus rejects the whole request). */
+ * A malformed request is PRIO3GPU_E_ARG (Janus rejects the whole request,
+ * AggregationJobInitializeReq::get_decoded at aggregator.rs:1586). */
 int prio3gpu_decode_agg_init_req(const uint8_t* msg, size_t len, int query_type,
                                  uint8_t* out_batch_id, uint64_t* out_agg_param,
                                  prio3gpu_prepare_init_view* views, size_t max_views,
                                  size_t* out_n);
+/* Helper: the request-level checks handle_aggregate_init_generic makes after decoding, each
+ * PRIO3GPU_E_INVALID_MESSAGE for the whole request:
+ *   two PrepareInits with the same report ID           (aggregator.rs:1588-1598)
+ *   an aggregation parameter other than Prio3's `()`   (aggregator.rs:1605: non-empty bytes). */
+int prio3gpu_check_agg_init_req(const uint8_t* msg, const prio3gpu_prepare_init_view* views,
+                                size_t n, uint64_t agg_param_len);
 /* Helper: pack the engine inputs of n PrepareInits (nonces n x 16, public shares, leader prep
- * shares).  Public share of the wrong length -> InvalidMessage; a message that is not
- * Initialize{prep share of the right length} -> VdafPrepError.  status in/out. */
+ * shares) and record each report's structural fault WITHOUT touching its status:
+ *   faults[i] = 8 InvalidMessage  public share of the wrong length        (aggregator.rs:1755-1768)
+ *             = 5 VdafPrepError   not Initialize{prep share of the right length}
+ *                                 (ping-pong, aggregator.rs:1775-1797 / error.rs:240-300)
+ *             = 0                 none.
+ * Janus reaches these checks only after HPKE open (3 / 4) and the plaintext / input-share decode
+ * (8) succeeded, so the caller applies faults to the reports whose status is still 0 after those
+ * stages (prio3gpu_apply_faults).  Rows of faulty reports are zeroed. */
 int prio3gpu_gather_prepare_inits(const prio3gpu_sizes* sizes, const uint8_t* msg,
                                   const prio3gpu_prepare_init_view* views, size_t n,
                                   uint8_t* nonces, uint8_t* public_shares,
-                                  uint8_t* leader_prep_shares, uint8_t* status);
+                                  uint8_t* leader_prep_shares, uint8_t* faults);
+/* status[i] = faults[i] for every report whose status is 0 (the precedence of the helper loop,
+ * aggregator.rs:1663-1797: HPKE config / decrypt, plaintext + input-share decode, public-share
+ * decode, ping-pong). */
+int prio3gpu_apply_faults(size_t n, const uint8_t* faults, uint8_t* status);
 /* HPKE-opened PlaintextInputShares (report i = plaintexts[offsets[i] .. offsets[i+1])) ->
  * n x input share (agg_id 0: leader, 1: helper).  Undecodable, duplicate extensions or wrong
  * payload length -> InvalidMessage.  status in/out. */

@@ -26,6 +26,18 @@ class Prio3GpuError(RuntimeError):
     pass
 
 
+class InvalidMessage(Prio3GpuError):
+    """The whole request is invalid (Janus `Error::InvalidMessage`, DAP "invalidMessage"):
+    duplicate report IDs, a non-empty Prio3 aggregation parameter (aggregator.rs:1588-1605)."""
+
+
+class EmptyAggregation(Prio3GpuError):
+    """An aggregation job without reports (Janus `Error::EmptyAggregation`, aggregator.rs:1851-1863)."""
+
+
+E_INVALID_MESSAGE = -7
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP engine for gfx950 into janus_amd/lib/libprio3gpu.so."""
     srcs = [CSRC / "engine.hip", CSRC / "codec.cpp", CSRC / "hpke.cpp"]
@@ -88,6 +100,8 @@ def _declare(lib):
         "prio3gpu_decode_agg_init_req": (c.c_int, [u8p, c.c_size_t, c.c_int, u8p, P, P, c.c_size_t,
                                                    c.POINTER(c.c_size_t)]),
         "prio3gpu_gather_prepare_inits": (c.c_int, [P, u8p, P, c.c_size_t, u8p, u8p, u8p, u8p]),
+        "prio3gpu_apply_faults": (c.c_int, [c.c_size_t, u8p, u8p]),
+        "prio3gpu_check_agg_init_req": (c.c_int, [u8p, P, c.c_size_t, c.c_uint64]),
         "prio3gpu_decode_plaintext_input_shares": (c.c_int, [P, u8p, P, c.c_size_t, c.c_int, u8p,
                                                              u8p]),
         "prio3gpu_encode_agg_job_resp": (c.c_int, [u8p, u8p, c.c_uint32, u8p, c.c_size_t, u8p,
@@ -135,6 +149,7 @@ EXPORTED = [
     "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
     "prio3gpu_prof_kernel_name", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
     "prio3gpu_last_error", "prio3gpu_unshard", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
+    "prio3gpu_apply_faults", "prio3gpu_check_agg_init_req",
     "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",
     "prio3gpu_encode_agg_init_req", "prio3gpu_decode_agg_job_resp", "prio3gpu_gather_helper_resps",
     "prio3gpu_hpke_open", "prio3gpu_hpke_seal", "prio3gpu_hpke_public_key",
@@ -160,4 +175,5 @@ def lib():
 def check(rc: int, what: str = "") -> None:
     if rc != 0:
         msg = lib().prio3gpu_last_error().decode(errors="replace")
-        raise Prio3GpuError(f"{what} failed ({rc}): {msg}")
+        cls = InvalidMessage if rc == E_INVALID_MESSAGE else Prio3GpuError
+        raise cls(f"{what} failed ({rc}): {msg}")

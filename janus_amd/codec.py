@@ -18,7 +18,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from ._lib import check, lib
+from ._lib import EmptyAggregation, InvalidMessage, check, lib  # noqa: F401 (re-exported)
 
 TIME_INTERVAL, FIXED_SIZE = 1, 2
 
@@ -77,6 +77,8 @@ class AggInitReq:
 
 
 def decode_agg_init_req(msg: bytes, query_type: int = TIME_INTERVAL) -> AggInitReq:
+    """Decode an AggregationJobInitializeReq (aggregator.rs:1586); Prio3GpuError for a malformed
+    request.  The helper then runs `check_agg_init_req`."""
     # no copy of the (up to hundreds of MB) request: bytes give a read-only view, a bytearray or
     # ndarray a writable one that aliases the caller's buffer
     raw = msg if isinstance(msg, np.ndarray) else np.frombuffer(msg, dtype=np.uint8)
@@ -93,12 +95,21 @@ def decode_agg_init_req(msg: bytes, query_type: int = TIME_INTERVAL) -> AggInitR
                       bid.tobytes() if query_type == FIXED_SIZE else None)
 
 
-def gather_prepare_inits(sizes, req: AggInitReq, status: Optional[np.ndarray] = None,
-                         lps_out: Optional[np.ndarray] = None):
-    """(nonces, public shares, leader prep shares, status) for prio3gpu_helper_init.  `lps_out`:
-    optional (>= n, prep_share) uint8 buffer (e.g. pinned host memory) for the prep shares."""
+def check_agg_init_req(req: AggInitReq) -> None:
+    """Helper request-level checks (aggregator.rs:1588-1605): raises `InvalidMessage` when two
+    PrepareInits carry the same report ID or the aggregation parameter is not Prio3's empty `()`."""
+    check(lib().prio3gpu_check_agg_init_req(_p(req.raw), req.views, req.n, len(req.agg_param)),
+          "aggregate-init request")
+
+
+def gather_prepare_inits(sizes, req: AggInitReq, lps_out: Optional[np.ndarray] = None):
+    """(nonces, public shares, leader prep shares, faults) for prio3gpu_helper_init.  `faults[i]`
+    is the status report i gets if it survives HPKE open and the plaintext decode (8: public share
+    of the wrong length, 5: not Initialize{prep share}); apply it with `apply_faults` after those
+    stages, which is Janus's precedence (aggregator.rs:1663-1797).  `lps_out`: optional
+    (>= n, prep_share) uint8 buffer (e.g. pinned host memory) for the prep shares."""
     n = req.n
-    st = np.zeros(n, np.uint8) if status is None else status
+    st = np.zeros(n, np.uint8)
     nonces = np.zeros((n, 16), np.uint8)
     pub = np.zeros((n, sizes.public_share), np.uint8)
     if lps_out is not None:
@@ -110,6 +121,13 @@ def gather_prepare_inits(sizes, req: AggInitReq, status: Optional[np.ndarray] = 
     check(lib().prio3gpu_gather_prepare_inits(ctypes.byref(sizes), _p(req.raw), req.views, n,
                                               _p(nonces), _p(pub), _p(lps), _p(st)), "gather")
     return nonces, pub, lps, st
+
+
+def apply_faults(status: np.ndarray, faults: np.ndarray) -> np.ndarray:
+    """status[i] = faults[i] where status[i] is still 0 (in place; returns status)."""
+    assert status.dtype == np.uint8 and faults.dtype == np.uint8 and len(status) == len(faults)
+    check(lib().prio3gpu_apply_faults(len(status), _p(faults), _p(status)), "apply faults")
+    return status
 
 
 def decode_plaintext_input_shares(sizes, plaintexts: Sequence[bytes], agg_id: int = 1,

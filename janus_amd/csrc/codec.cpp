@@ -28,9 +28,11 @@
 #include <cstdint>
 #include <cstring>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/prio3gpu.h"
+#include "errors.h"
 
 namespace {
 
@@ -149,20 +151,50 @@ int prio3gpu_decode_agg_init_req(const uint8_t* msg, size_t len, int query_type,
   return 0;
 }
 
+int prio3gpu_check_agg_init_req(const uint8_t* msg, const prio3gpu_prepare_init_view* views,
+                                size_t n, uint64_t agg_param_len) {
+  if (n && (!msg || !views)) return PRIO3GPU_E_ARG;
+  // Duplicate report IDs abort the whole request (aggregator.rs:1588-1598).  Sorting the IDs as
+  // big-endian 128-bit keys is O(n log n) whatever IDs an adversarial leader picks.
+  std::vector<std::pair<uint64_t, uint64_t>> ids(n);
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t* id = msg + views[i].report_id_off;
+    uint64_t hi = 0, lo = 0;
+    for (int b = 0; b < 8; ++b) hi = (hi << 8) | id[b];
+    for (int b = 8; b < 16; ++b) lo = (lo << 8) | id[b];
+    ids[i] = {hi, lo};
+  }
+  std::sort(ids.begin(), ids.end());
+  for (size_t i = 1; i < n; ++i) {
+    if (ids[i] == ids[i - 1]) {
+      p3g::set_error("aggregate request contains duplicate report IDs");
+      return PRIO3GPU_E_INVALID_MESSAGE;
+    }
+  }
+  // A::AggregationParam::get_decoded (aggregator.rs:1605): Prio3's aggregation parameter is `()`,
+  // whose decoding accepts only the empty byte string.
+  if (agg_param_len != 0) {
+    p3g::set_error("aggregation parameter must be empty for Prio3 (got %llu bytes)",
+                   (unsigned long long)agg_param_len);
+    return PRIO3GPU_E_INVALID_MESSAGE;
+  }
+  return 0;
+}
+
 int prio3gpu_gather_prepare_inits(const prio3gpu_sizes* sz, const uint8_t* msg,
                                   const prio3gpu_prepare_init_view* views, size_t n,
                                   uint8_t* nonces, uint8_t* public_shares,
-                                  uint8_t* leader_prep_shares, uint8_t* status) {
-  if (!sz || (n && (!msg || !views || !nonces || !status))) return PRIO3GPU_E_ARG;
+                                  uint8_t* leader_prep_shares, uint8_t* faults) {
+  if (!sz || (n && (!msg || !views || !nonces || !faults))) return PRIO3GPU_E_ARG;
   // Reports are independent: large batches (SumVec: 2.9 KB of leader prep share each) are copied
-  // on up to 8 threads, each output row written once (zeroed only for a rejected report).
+  // on up to 8 threads, each output row written once (zeroed only for a faulty report).
   auto run = [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
       const prio3gpu_prepare_init_view& v = views[i];
       memcpy(nonces + 16 * i, msg + v.report_id_off, 16);
-      uint8_t st = status[i];
-      if (st == PRIO3GPU_OK && v.public_share_len != sz->public_share) st = PRIO3GPU_INVALID_MESSAGE;
-      if (st == PRIO3GPU_OK && (v.message_type != 0 || v.prep_share_len != sz->prep_share))
+      uint8_t st = PRIO3GPU_OK;
+      if (v.public_share_len != sz->public_share) st = PRIO3GPU_INVALID_MESSAGE;
+      else if (v.message_type != 0 || v.prep_share_len != sz->prep_share)
         st = PRIO3GPU_VDAF_PREP_ERROR;
       const bool ok = st == PRIO3GPU_OK;
       if (public_shares && sz->public_share) {
@@ -175,7 +207,7 @@ int prio3gpu_gather_prepare_inits(const prio3gpu_sizes* sz, const uint8_t* msg,
         if (ok) memcpy(d, msg + v.prep_share_off, sz->prep_share);
         else memset(d, 0, sz->prep_share);
       }
-      status[i] = st;
+      faults[i] = st;
     }
   };
   const size_t bytes = n * (size_t)(16 + sz->public_share + sz->prep_share);
@@ -190,6 +222,13 @@ int prio3gpu_gather_prepare_inits(const prio3gpu_sizes* sz, const uint8_t* msg,
     pool.emplace_back(run, std::min(n, t * per), std::min(n, (t + 1) * per));
   run(0, std::min(n, per));
   for (auto& th : pool) th.join();
+  return 0;
+}
+
+int prio3gpu_apply_faults(size_t n, const uint8_t* faults, uint8_t* status) {
+  if (n && (!faults || !status)) return PRIO3GPU_E_ARG;
+  for (size_t i = 0; i < n; ++i)
+    if (status[i] == PRIO3GPU_OK) status[i] = faults[i];
   return 0;
 }
 

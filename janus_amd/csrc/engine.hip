@@ -12,16 +12,17 @@
 #include <vector>
 
 #include "../../include/prio3gpu.h"
+#include "errors.h"
 #include "prio3_kernels.h"
 #include "fpvec_kernels.h"
 
 using namespace p3g;
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-void set_err(const char* fmt, ...) {
+void p3g::set_error(const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -29,6 +30,10 @@ void set_err(const char* fmt, ...) {
   va_end(ap);
   g_err = buf;
 }
+
+namespace {
+
+#define set_err p3g::set_error
 
 #define HIPCHK(x)                                                                 \
   do {                                                                            \

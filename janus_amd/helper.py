@@ -3,14 +3,19 @@
 minus the datastore transaction (out of scope).
 
 Per aggregation job (one AggregationJobInitializeReq):
-  1. decode the request and gather the engine inputs          codec.cpp   (aggregator.rs:1561-1612)
-  2. HPKE-open every encrypted input share on host threads    hpke.cpp    (aggregator.rs:1634-1700)
-  3. decode the PlaintextInputShares into the input-share array          (aggregator.rs:1702-1768)
+  1. decode the request; request-level checks: duplicate report IDs and a non-empty aggregation
+     parameter fail the whole request (`InvalidMessage`, aggregator.rs:1588-1605), an empty job
+     fails it too (`EmptyAggregation`, aggregator.rs:1851-1863); gather the engine inputs and
+     each report's structural faults                                 codec.cpp   (aggregator.rs:1561-1612)
+  2. HPKE-open every encrypted input share on host threads            hpke.cpp    (aggregator.rs:1634-1700)
+  3. decode the PlaintextInputShares into the input-share array, then apply the structural
+     faults to the reports still OK (Janus's precedence: HPKE 3/4, plaintext/input share 8,
+     public share 8, ping-pong 5)                                                 (aggregator.rs:1702-1797)
   4. prio3gpu_helper_init: prepare_init + decide + prepare_next + accumulate on the GPU, and
      prio3gpu_agg_update_reports: report-ID checksum + client-timestamp interval per batch
-                                                                          (aggregator.rs:1775-1819,
-                                                                           accumulator.rs:76-122)
-  5. encode the AggregationJobResp                                        (aggregator.rs:1811-1848)
+                                                                                  (aggregator.rs:1775-1819,
+                                                                                   accumulator.rs:76-122)
+  5. encode the AggregationJobResp                                                (aggregator.rs:1811-1848)
 
 `handle_jobs` pipelines a stream of jobs: while the GPU runs job k (step 4, the ctypes call
 releases the GIL and blocks on the engine's stream), a host worker thread runs steps 1-3 of job
@@ -20,6 +25,7 @@ reference's mapping: status 3 HpkeUnknownConfigId, 4 HpkeDecryptError, 5 VdafPre
 """
 from __future__ import annotations
 
+import threading
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence
@@ -28,6 +34,7 @@ import numpy as np
 
 from . import codec as C
 from . import hpke
+from ._lib import EmptyAggregation
 from .prio3 import AggregateShares, Prio3Gpu
 
 
@@ -41,6 +48,46 @@ class _Opened:
     status: np.ndarray
     slots: Optional[np.ndarray]
     times: np.ndarray
+    buf: int = -1  # index of the pinned staging buffer holding leader_prep (-1: none)
+
+
+class _PinnedPool:
+    """Pinned host buffers for the leader prep shares of jobs in flight.  A buffer is owned by one
+    opened job from `acquire` until `release` (after its GPU stage), so any number of jobs may be
+    opened ahead of preparation without one overwriting another's rows."""
+
+    def __init__(self, row_bytes: int):
+        self.row_bytes = row_bytes
+        self._bufs: List[np.ndarray] = []
+        self._keep: List[object] = []
+        self._busy: List[bool] = []
+        self._lock = threading.Lock()
+
+    def acquire(self, n: int):
+        import torch
+        if n == 0 or not torch.cuda.is_available():
+            return -1, None
+        with self._lock:
+            for k, b in enumerate(self._bufs):
+                if not self._busy[k] and b.shape[0] >= n:
+                    self._busy[k] = True
+                    return k, b
+            t = torch.empty((max(n, 1024), self.row_bytes), dtype=torch.uint8, pin_memory=True)
+            self._keep.append(t)
+            self._bufs.append(t.numpy())
+            self._busy.append(True)
+            return len(self._bufs) - 1, self._bufs[-1]
+
+    def release(self, k: int):
+        if k < 0:
+            return
+        with self._lock:
+            assert self._busy[k], "staging buffer released twice"
+            self._busy[k] = False
+
+    def clear(self):
+        with self._lock:
+            self._bufs, self._keep, self._busy = [], [], []
 
 
 class HelperAggregateInit:
@@ -59,52 +106,48 @@ class HelperAggregateInit:
         self.batch_slot_of = batch_slot_of
         self._state = None
         self._cap = 0
-        # two pinned staging buffers for the leader prep shares (the largest per-report input,
-        # 2,896 B for SumVec): job k+1 is gathered into one while job k's is copied to the GPU
-        # from the other; pageable memory would make that copy the slowest step.
-        self._pinned: List[Optional[np.ndarray]] = [None, None]
-        self._pin_keep: List[object] = [None, None]
-        self._next_buf = 0
+        # pinned staging for the leader prep shares (the largest per-report input, 2,896 B for
+        # SumVec): job k+1 is gathered into one buffer while job k's is copied to the GPU from
+        # another; pageable memory would make that copy the slowest step.
+        self._pinned = _PinnedPool(vdaf.sizes.prep_share)
 
     def open(self, req_bytes: bytes) -> _Opened:
-        """Steps 1-3 (host only)."""
+        """Steps 1-3 (host only).  Raises InvalidMessage / EmptyAggregation for the request."""
         s = self.vdaf.sizes
         req = C.decode_agg_init_req(req_bytes, self.query_type)
-        nonces, pub, lps, st = C.gather_prepare_inits(s, req, lps_out=self._staging(req.n))
-        pts, offs, st = hpke.open_report_shares(self.task_id, req, self.task_keys,
-                                                self.global_keys, st, self.hpke_threads)
-        hin, st = C.decode_plaintext_input_shares_raw(s, pts, offs, 1, st)
-        slots = None
-        if self.batch_slot_of is not None:
-            slots = np.ascontiguousarray(self.batch_slot_of(req.times()), np.uint32)
-        return _Opened(req.n, nonces, pub, lps, hin, st, slots, req.times())
-
-    def _staging(self, n: int) -> Optional[np.ndarray]:
-        """Pinned buffer for the next job's leader prep shares (alternating), or None off-GPU."""
-        import torch
-        if n == 0 or not torch.cuda.is_available():
-            return None
-        k = self._next_buf
-        self._next_buf ^= 1
-        buf = self._pinned[k]
-        ps = self.vdaf.sizes.prep_share
-        if buf is None or buf.shape[0] < n:
-            t = torch.empty((max(n, 2 * (0 if buf is None else buf.shape[0])), ps),
-                            dtype=torch.uint8, pin_memory=True)
-            self._pin_keep[k] = t
-            self._pinned[k] = buf = t.numpy()
-        return buf
+        C.check_agg_init_req(req)
+        if req.n == 0:
+            raise EmptyAggregation("aggregation job contains no reports")
+        k, buf = self._pinned.acquire(req.n)
+        try:
+            nonces, pub, lps, faults = C.gather_prepare_inits(s, req, lps_out=buf)
+            pts, offs, st = hpke.open_report_shares(self.task_id, req, self.task_keys,
+                                                    self.global_keys, None, self.hpke_threads)
+            hin, st = C.decode_plaintext_input_shares_raw(s, pts, offs, 1, st)
+            C.apply_faults(st, faults)
+            slots = None
+            times = req.times()
+            if self.batch_slot_of is not None:
+                slots = np.ascontiguousarray(self.batch_slot_of(times), np.uint32)
+        except BaseException:
+            self._pinned.release(k)
+            raise
+        return _Opened(req.n, nonces, pub, lps, hin, st, slots, times, k)
 
     def prepare(self, o: _Opened, agg: AggregateShares) -> bytes:
         """Steps 4-5 (GPU + encode)."""
-        if o.n > self._cap:
-            if self._state is not None:
-                self._state.close()
-            self._cap = max(o.n, 2 * self._cap)
-            self._state = self.vdaf.new_state(1, self._cap)
-        msgs, st = self.vdaf.helper_init(self._state, o.nonces, o.public, o.helper_in,
-                                         o.leader_prep, agg=agg, batch_slots=o.slots,
-                                         status=o.status)
+        try:
+            if o.n > self._cap:
+                if self._state is not None:
+                    self._state.close()
+                self._cap = max(o.n, 2 * self._cap)
+                self._state = self.vdaf.new_state(1, self._cap)
+            msgs, st = self.vdaf.helper_init(self._state, o.nonces, o.public, o.helper_in,
+                                             o.leader_prep, agg=agg, batch_slots=o.slots,
+                                             status=o.status)
+        finally:
+            self._pinned.release(o.buf)  # helper_init returns after its stream has synchronised
+            o.buf = -1
         # Accumulator::update bookkeeping: report-ID checksum + client-timestamp interval
         agg.update_reports(o.nonces, o.times, st, o.slots)
         return C.encode_agg_job_resp(o.nonces, msgs, self.vdaf.sizes.prep_msg, st)
@@ -130,5 +173,4 @@ class HelperAggregateInit:
         if self._state is not None:
             self._state.close()
             self._state = None
-        self._pinned = [None, None]
-        self._pin_keep = [None, None]
+        self._pinned.clear()

@@ -53,15 +53,18 @@ def test_decode_agg_init_req_kat(qt, key):
 def test_gather_prepare_inits_error_mapping():
     """Report 0 (Initialize, 6-byte prep share, empty public share) is accepted; report 1 has a
     4-byte public share (InvalidMessage when the VDAF expects none) and carries Finish instead of
-    Initialize (VdafPrepError once its public share decodes)."""
+    Initialize (VdafPrepError once its public share decodes).  The gather only records these
+    faults; they apply to reports still OK after HPKE (test_helper_requests.py)."""
     k = KATS["agg_init_req"]
     req = C.decode_agg_init_req(h(k["time_interval"]))
-    nonces, pub, lps, st = C.gather_prepare_inits(_sizes(), req)
-    assert list(st) == [0, 8]
+    nonces, pub, lps, faults = C.gather_prepare_inits(_sizes(), req)
+    assert list(faults) == [0, 8]
     assert nonces[0].tobytes() == h(k["reports"][0]["report_id"])
     assert lps[0].tobytes() == h("303132333435")
-    _, _, _, st = C.gather_prepare_inits(_sizes(public_share=4), req)
-    assert list(st) == [8, 5]
+    _, _, _, faults = C.gather_prepare_inits(_sizes(public_share=4), req)
+    assert list(faults) == [8, 5]
+    st = np.array([4, 0], np.uint8)  # report 0's HPKE open failed first
+    assert list(C.apply_faults(st, faults)) == [4, 5]
 
 
 def test_encode_agg_init_req_matches_kat_bytes():
@@ -155,9 +158,12 @@ def test_message_round_trip_through_engine(name):
     # helper
     d = C.decode_agg_init_req(req)
     assert d.n == b.n and (d.times() == np.arange(b.n)).all()
-    nonces, pub, lps, st = C.gather_prepare_inits(s, d)
+    C.check_agg_init_req(d)
+    nonces, pub, lps, faults = C.gather_prepare_inits(s, d)
+    st = np.zeros(d.n, np.uint8)
     st[3] = 4  # report 3's HPKE open failed on the CPU stage: PrepareError::HpkeDecryptError
     hin, st = C.decode_plaintext_input_shares(s, [ct[2] for ct in d.hpke_ciphertexts()], 1, st)
+    C.apply_faults(st, faults)
     hagg = v.new_aggregate(1)
     msgs, hst = v.helper_init(hs, nonces, pub, hin, lps, agg=hagg, status=st)
     resp = C.encode_agg_job_resp(nonces, msgs, s.prep_msg, hst)

@@ -97,10 +97,11 @@ def main():
     req = C.decode_agg_init_req(reqs[0])
     stages["decode_req"] = time.perf_counter() - t
     t = time.perf_counter()
-    nonces_, pub_, lps_, st_ = C.gather_prepare_inits(s, req)
-    stages["gather"] = time.perf_counter() - t
+    C.check_agg_init_req(req)
+    nonces_, pub_, lps_, faults_ = C.gather_prepare_inits(s, req)
+    stages["check_gather"] = time.perf_counter() - t
     t = time.perf_counter()
-    pts, offs, st_ = H.open_report_shares(task_id, req, [tk], [], st_, args.threads)
+    pts, offs, st_ = H.open_report_shares(task_id, req, [tk], [], None, args.threads)
     stages["hpke_open"] = time.perf_counter() - t
     t = time.perf_counter()
     C.decode_plaintext_input_shares_raw(s, pts, offs, 1, st_)
