@@ -41,6 +41,77 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 # SURVEY.md §8(d) declared cost model: 7,440 int32 VALU ops per Keccak-f[1600]; 36 per F128 mul.
 OPS_PER_PERM = 7440
+# VALU issue rate: 256 CU x 4 SIMD x 2.4 GHz, a wave64 instruction every 2 cycles on a 32-lane SIMD
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
+# Measured register-only Keccak-f[1600] ceiling of one MI355X (tools/mb_keccak_occ.hip,
+# profiles/microbench_keccak_mem_r01.log: 10.3-10.8 G permutations/s at 2-6 waves/SIMD)
+KECCAK_CEILING = 10.8e9
+PMC_ROUND = "r02"
+
+
+def cpu_threads(requested=0):
+    """Threads for the CPU legs: the host CPUs this process may run on (affinity), capped by the
+    cgroup CPU quota and by OMP_NUM_THREADS when set (a GPU box grants a 16-CPU share of a larger
+    machine and announces it that way)."""
+    if requested > 0:
+        return requested
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    try:
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def host_cpu_info():
+    info = {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        info["cgroup_cpu_max"] = open("/sys/fs/cgroup/cpu.max").read().strip()
+    except OSError:
+        pass
+    return info
+
+
+def load_pmc(config):
+    """Per-kernel PMC summary of the same bench command (tools/profile_round.sh), this round's
+    first: {"source": path, "kernels": {name: {...}}}."""
+    for path in (os.path.join(ROOT, "profiles", PMC_ROUND, f"pmc_{config}.json"),
+                 os.path.join(ROOT, "profiles", f"pmc_{config}.json")):
+        if os.path.exists(path):
+            try:
+                return {"source": os.path.relpath(path, ROOT), "kernels": json.load(open(path))}
+            except (OSError, ValueError):
+                pass
+    return {}
+
+
+def flp_wires_bytes_per_report(s):
+    """Algorithmic HBM bytes of k_flp_wires per report (ParallelSum types): the measurement share
+    once, the weight row W = MM[calls] | LM[calls] | RP[c] | B0[c] | B1[c] | gsum, and the
+    2c wire values written into the prep share."""
+    es = s.field_size
+    arity = s.verifier_len - 2
+    c = arity // 2
+    calls = -(-s.meas_len // c)
+    w_len = 2 * calls + 3 * c + 1
+    return (s.meas_len + w_len + arity) * es
 
 
 def perms_per_report(kind_name, sizes):
@@ -70,7 +141,8 @@ def main():
     ap.add_argument("--unique", type=int, default=0, help="CPU-baseline sample size (reports)")
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: the host CPUs this process may use)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="leader and helper on separate contexts/streams, prepare_init concurrent")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
@@ -93,11 +165,15 @@ def main():
     dev = torch.device("cuda", local_rank)
     dist = None
     if world > 1:
+        # Host-side coordination only (barriers, max-over-ranks timing, the RCCL unique id):
+        # gloo.  The one RCCL communicator of the process is the engine's own (prio3gpu_comm),
+        # which carries the data-path collective; torch does not create a second one.
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")
 
     from janus_amd import _lib
     from janus_amd._lib import check, lib
+    from janus_amd.parallel import shard_range
     from janus_amd.prio3 import Comm, Prio3Gpu
     from oracle.ref import Prio3Ref
 
@@ -122,7 +198,8 @@ def main():
     # checked against the C restatement's own shard before anything is timed.
     ref = Prio3Ref(kind, vk, bits, length, chunk)
     t0 = time.time()
-    syn = ref.synth(cfg_id, rank * B, B, threads=args.gen_threads)
+    lo, hi = shard_range(B * world, world, rank)  # weak scaling: B reports per rank
+    syn = ref.synth(cfg_id, lo, hi - lo, threads=args.gen_threads)
     d_nonces = torch.from_numpy(syn["nonces"]).to(dev)
     d_meas = torch.from_numpy(syn["meas"].view(np.int64)).to(dev)
     d_rand = torch.from_numpy(syn["rand"]).to(dev)
@@ -137,7 +214,7 @@ def main():
     del d_rand
     gen_s = time.time() - t0
     U = min(U, B)  # CPU-baseline sample size
-    chk = ref.gen(cfg_id, rank * B, min(U, 64), threads=args.gen_threads)
+    chk = ref.gen(cfg_id, lo, min(U, 64), threads=args.gen_threads)
     k = chk["nonces"].shape[0]
     assert np.array_equal(d_lin[:k].cpu().numpy(), chk["leader_in"]), "GPU shard != C shard"
     assert np.array_equal(d_hin[:k].cpu().numpy(), chk["helper_in"]), "GPU shard != C shard"
@@ -250,7 +327,7 @@ def main():
         ctxs += [wk.v._ctx] + ([wk.hv._ctx] if wk.hv is not wk.v else [])
     for cx in ctxs:
         check(L.prio3gpu_prof_enable(cx, 1), "prof")
-        L.prio3gpu_prof_read(cx, (ctypes.c_double * 16)(), (ctypes.c_uint64 * 16)(), 16)
+        L.prio3gpu_prof_read(cx, (ctypes.c_double * 64)(), (ctypes.c_uint64 * 64)(), 64)
 
     def barrier():
         torch.cuda.synchronize()
@@ -266,9 +343,9 @@ def main():
     elapsed = time.perf_counter() - t0
     kt = {}
     for cx in ctxs:
-        ms = (ctypes.c_double * 16)()
-        nl = (ctypes.c_uint64 * 16)()
-        nk = L.prio3gpu_prof_read(cx, ms, nl, 16)
+        ms = (ctypes.c_double * 64)()
+        nl = (ctypes.c_uint64 * 64)()
+        nk = L.prio3gpu_prof_read(cx, ms, nl, 64)
         for i in range(nk):
             if nl[i]:
                 name = L.prio3gpu_prof_kernel_name(i).decode()
@@ -276,7 +353,7 @@ def main():
                 kt[name] = (a + ms[i], b + nl[i])
         check(L.prio3gpu_prof_enable(cx, 0), "prof")
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -320,8 +397,33 @@ def main():
                                np.uint8).reshape(B, 32)
             x = np.bitwise_xor.reduce(dg, axis=0) if total_steps % 2 else np.zeros(32, np.uint8)
             assert cks[0][0] == x.tobytes(), "report-ID checksum != SHA-256 XOR"
-    parity = ("unshard(aggregate) == plaintext sum; report-ID checksums == hashlib; "
-              "status all ok")
+
+    # byte-level gate: the first G reports of this rank through the same GPU path
+    # (leader prepare_init, helper_init, leader prepare_next + accumulate) and through the C
+    # restatement of prio 0.15.1: both aggregators' aggregate-share bytes and counts identical.
+    G = min(U, B)
+    nthr = cpu_threads(args.cpu_threads)
+    cn = d_nonces[:G].cpu().numpy()
+    cp = d_pub[:G].cpu().numpy() if d_pub is not None else np.zeros((G, 0), np.uint8)
+    cl = d_lin[:G].cpu().numpy()
+    ch = d_hin[:G].cpu().numpy()
+    gv = workers[0].v
+    gls, ghs = gv.new_state(0, G), gv.new_state(1, G)
+    glagg, ghagg = gv.new_aggregate(1), gv.new_aggregate(1)
+    gpub = d_pub[:G] if d_pub is not None else None
+    glp, glst = gv.prepare_init(gls, d_nonces[:G], gpub, d_lin[:G])
+    gmsgs, ghst = gv.helper_init(ghs, d_nonces[:G], gpub, d_hin[:G], glp, agg=ghagg)
+    gv.prepare_next(gls, gmsgs, glst, want_output_shares=False, agg=glagg)
+    ref_res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=False)
+    (gla, glc), (gha, ghc) = glagg.read(0), ghagg.read(0)
+    assert glc == ghc == ref_res["count"] == G, (glc, ghc, ref_res["count"], G)
+    assert gla == ref_res["agg_l"].tobytes(), "leader aggregate share != C restatement"
+    assert gha == ref_res["agg_h"].tobytes(), "helper aggregate share != C restatement"
+    for o in (gls, ghs, glagg, ghagg):
+        o.close()
+    parity = (f"aggregate-share bytes == C restatement (both aggregators, {G} reports/rank "
+              f"through the product path); unshard(aggregate) == plaintext sum over every timed "
+              f"step; report-ID checksums == hashlib; status all ok")
 
     # ---- helper-only variant (the A1 path alone: helper_init + bookkeeping), SURVEY §8(d) -------
     helper_only = None
@@ -345,7 +447,7 @@ def main():
         barrier()
         h_el = time.perf_counter() - th0
         if dist is not None:
-            t = torch.tensor([h_el], dtype=torch.float64, device=dev)
+            t = torch.tensor([h_el], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             h_el = float(t.item())
         assert int(d_hst.max().item()) == 0 and hagg2.read(0)[1] == (args.steps + 1) * wk.n
@@ -366,53 +468,77 @@ def main():
     avg_launch_s = dms / 1e3 / dlaunch
     # B / W reports per launch; k_jr runs once per aggregator and worker (2 W launches per step)
     nlaunch = bounds[1] - bounds[0]
+    pmc = load_pmc(args.config)
     if dname in perms and perms[dname]:
         ops = perms[dname] * nlaunch * OPS_PER_PERM
         achieved = ops / avg_launch_s / 1e12
+        perm_rate = perms[dname] * nlaunch / avg_launch_s
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
                 "kernel": dname, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                 "model": f"{perms[dname]} Keccak-f[1600]/report x {OPS_PER_PERM} int32 ops "
-                         f"(SURVEY §8(d)) x {nlaunch} reports/launch"}
+                         f"(SURVEY §8(d)) x {nlaunch} reports/launch",
+                "keccak_perms_per_s": round(perm_rate, 1),
+                # vs the measured register-only Keccak-f ceiling of this chip (tools/mb_keccak_occ.hip)
+                "keccak_ceiling_perms_per_s": KECCAK_CEILING,
+                "keccak_ceiling_frac": round(perm_rate / KECCAK_CEILING, 4),
+                "algorithmic_hbm_bytes_per_launch": (
+                    nlaunch * s.meas_len * s.field_size if dname == "k_jr" else
+                    nlaunch * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand"
+                    else None)}
     else:
         roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": None, "traffic": None, "kernel": dname,
                 "avg_launch_ms": round(avg_launch_s * 1e3, 3)}
-    if dname in perms and perms[dname]:
-        perm_rate = perms[dname] * nlaunch / avg_launch_s
-        roof["keccak_perms_per_s"] = round(perm_rate, 1)
-        roof["algorithmic_hbm_bytes_per_launch"] = (
-            nlaunch * s.meas_len * s.field_size if dname == "k_jr" else
-            nlaunch * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand" else None)
-    prof_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
-    if os.path.exists(prof_path):  # PMC pass of the same command (tools/profile_round.sh)
-        try:
-            pm = json.load(open(prof_path)).get(dname, {})
-            roof["traffic"] = pm.get("hbm_bytes_per_launch")
-            if pm.get("SQ_INSTS_VALU") and dname in perms and perms[dname]:
-                # instructions per lane-report: per-wave count / reports per wave (64)
+    pm = pmc.get("kernels", {}).get(dname)
+    if pm:  # PMC passes of the same command (tools/profile_round.sh), per launch
+        roof["traffic"] = pm.get("hbm_bytes_per_launch")
+        roof["pmc_source"] = pmc["source"]
+        if pm.get("SQ_INSTS_VALU"):
+            # wave-instructions issued / (launch time x the chip's VALU issue rate)
+            roof["valu_issue_frac"] = round(pm["SQ_INSTS_VALU"] / (pm["avg_ms"] / 1e3)
+                                            / VALU_ISSUE_PEAK, 4)
+            if dname in perms and perms[dname]:
                 roof["valu_insts_per_perm"] = round(pm["valu_insts_per_wave"] / perms[dname], 1)
-        except Exception:
-            pass
+    # the HBM-bound kernel of the step: the FLP wire pass streams each measurement share once
+    hbm_k = "k_flp_wires"
+    if hbm_k in kt and kt[hbm_k][1]:
+        hms, hl = kt[hbm_k]
+        h_avg = hms / 1e3 / hl
+        alg = nlaunch * flp_wires_bytes_per_report(s)
+        hb = {"kernel": hbm_k, "avg_launch_ms": round(h_avg * 1e3, 3),
+              "algorithmic_bytes_per_launch": alg,
+              "achieved": round(alg / h_avg / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(alg / h_avg / 1e9 / HBM_PEAK_GBS, 4), "traffic": None}
+        hp = pmc.get("kernels", {}).get(hbm_k)
+        if hp and hp.get("hbm_bytes_per_launch"):
+            hb["traffic"] = hp["hbm_bytes_per_launch"]
+            hb["traffic_over_algorithmic"] = round(hp["hbm_bytes_per_launch"] / alg, 3)
+        roof["hbm"] = hb
 
     # ---- CPU baseline: C restatement of prio 0.15.1, bounded sample, rank 0 at N = 1 -----------
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        cn = d_nonces[:U].cpu().numpy()
-        cp = d_pub[:U].cpu().numpy() if d_pub is not None else np.zeros((U, 0), np.uint8)
-        cl = d_lin[:U].cpu().numpy()
-        ch = d_hin[:U].cpu().numpy()
         done, t0 = 0, time.perf_counter()
         while True:
             res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=False)
-            assert res["count"] == U
-            done += U
+            assert res["count"] == G
+            done += G
             if time.perf_counter() - t0 >= args.cpu_seconds:
                 break
         cpu_s = time.perf_counter() - t0
+        # one thread: Janus's per-report loop inside one aggregation job (aggregator.rs:1613)
+        n1 = min(G, 256)
+        done1, t1 = 0, time.perf_counter()
+        while True:
+            r1 = ref.prepare_batch(cn[:n1], cp[:n1], cl[:n1], ch[:n1], threads=1, outputs=False)
+            assert r1["count"] == n1
+            done1 += n1
+            if time.perf_counter() - t1 >= max(2.0, args.cpu_seconds / 4):
+                break
+        cpu1_s = time.perf_counter() - t1
         # the CPU restatement's aggregate over the sample == plaintext sum of the sample
-        sm = syn["meas"][:U]
+        sm = syn["meas"][:G]
         if kind == 2:
             sp = [int(x) for x in sm.sum(axis=0, dtype=np.uint64)]
         elif kind == 3:
@@ -422,16 +548,19 @@ def main():
         assert vdaf.unshard([res["agg_l"].tobytes(), res["agg_h"].tobytes()]) == sp
         cpu = {"value": round(done / cpu_s, 2), "unit": "reports/s", "cores": nthr,
                "kind": "port",
-               "sample": f"{done} report preparations ({U} distinct reports, repeated) leader+helper "
-                         f"prepare+aggregate, {nthr} threads, {cpu_s:.1f} s; C restatement of "
-                         f"prio 0.15.1 (reference not buildable)"}
+               "one_thread": round(done1 / cpu1_s, 2),
+               "cpu_model": cpu_model(),
+               "host_cpus": host_cpu_info(),
+               "sample": f"{done} report preparations ({G} distinct reports, repeated) leader+helper "
+                         f"prepare+aggregate on {nthr} threads in {cpu_s:.1f} s, and {done1} on "
+                         f"1 thread in {cpu1_s:.1f} s; C restatement of prio 0.15.1 (the "
+                         f"reference's Rust path is not buildable here)"}
 
     # ---- HPKE open on host threads (excluded from `value`, reported separately: SURVEY §8(d)) --
     hpke_rep = None
     if rank == 0 and world == 1 and args.hpke:
         from janus_amd import codec as C
         from janus_amd import hpke as H
-        nthr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         nh = min(U, 8192)
         kp = H.generate_hpke_config_and_private_key(1)
         info = H.application_info(H.Label.INPUT_SHARE, H.ROLE_CLIENT, H.ROLE_HELPER)

@@ -202,6 +202,26 @@ int prio3gpu_shard(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const uint8_
                    const uint64_t* measurements, const uint8_t* rand, uint8_t* out_public,
                    uint8_t* out_leader, uint8_t* out_helper);
 
+/* BatchAggregation::merged_with (aggregator_core/src/datastore/models.rs:962-991) on host
+ * buffers: the merge Janus applies to the batch-aggregation shards of a batch at collection
+ * (aggregate_share.rs:47-65) and prio3gpu_agg_allreduce applies to the per-GPU partials.
+ *   aggregate_share  dst += src elementwise mod p (Aggregatable::merge); output_len elements of
+ *                    field_size (8: Field64, 16: Field128) canonical LE bytes; both NULL: skipped
+ *   report_count     dst += src
+ *   checksum         dst ^= src (ReportIdChecksum::combined_with, core/src/report_id.rs:18-44)
+ *   interval         Interval::merge (core/src/time.rs:289-302): a zero-duration interval is
+ *                    empty and yields the other; else [min start, max end).
+ * Host only (no GPU).  PRIO3GPU_E_ARG on a non-canonical share element or interval overflow. */
+typedef struct prio3gpu_batch_aggregation {
+  uint8_t* aggregate_share;
+  uint64_t report_count;
+  uint8_t checksum[32];
+  uint64_t interval_start, interval_duration;
+} prio3gpu_batch_aggregation;
+int prio3gpu_batch_aggregation_merge(uint32_t field_size, size_t output_len,
+                                     prio3gpu_batch_aggregation* dst,
+                                     const prio3gpu_batch_aggregation* src);
+
 /* Multi-GPU merge of per-GPU partial aggregates (one process per GPU).  RCCL all-gather of the
  * raw field-element bytes over xGMI, then a mod-p add kernel (RCCL sum is neither modular nor
  * 128-bit).  Counts are summed with an RCCL uint64 all-reduce.
@@ -221,6 +241,14 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg*
 int prio3gpu_prof_enable(prio3gpu_ctx* ctx, int on);
 int prio3gpu_prof_read(prio3gpu_ctx* ctx, double* ms, uint64_t* launches, int max_kernels);
 const char* prio3gpu_prof_kernel_name(int kernel_id);
+
+/* TEST ONLY.  The XOF squeeze every kernel runs (prio `into_field_vec`, reached through
+ * XofShake128::next_vec: ES-byte LE chunks, reject >= p) over caller-crafted rate blocks instead
+ * of Keccak output: blocks[25 i .. 25 i + 25) is the state after the i-th permutation (words
+ * 0..20 are the 168-byte rate block).  field_size 8 or 16; exact != 0 forces the per-element path
+ * (as PRIO3GPU_EXACT_SQUEEZE=1 does in the real kernels).  Runs on the current HIP device. */
+int prio3gpu_test_squeeze(int field_size, const uint64_t* blocks, size_t nblocks, uint32_t n,
+                          uint8_t* out, int exact);
 
 /* Device memory helpers (bench / tests that stage inputs in HBM without torch). */
 int prio3gpu_dev_alloc(prio3gpu_ctx* ctx, size_t bytes, void** out);

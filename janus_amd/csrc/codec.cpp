@@ -225,6 +225,59 @@ int prio3gpu_gather_prepare_inits(const prio3gpu_sizes* sz, const uint8_t* msg,
   return 0;
 }
 
+int prio3gpu_batch_aggregation_merge(uint32_t field_size, size_t output_len,
+                                     prio3gpu_batch_aggregation* dst,
+                                     const prio3gpu_batch_aggregation* src) {
+  typedef unsigned __int128 u128;
+  if (!dst || !src || (field_size != 8 && field_size != 16) ||
+      (!dst->aggregate_share != !src->aggregate_share)) {
+    p3g::set_error("batch_aggregation_merge: bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  // Interval::merge (core/src/time.rs:289-302)
+  uint64_t start = dst->interval_start, dur = dst->interval_duration;
+  if (dur == 0) {
+    start = src->interval_start;
+    dur = src->interval_duration;
+  } else if (src->interval_duration != 0) {
+    u128 e0 = (u128)dst->interval_start + dst->interval_duration;
+    u128 e1 = (u128)src->interval_start + src->interval_duration;
+    const u128 end = e0 > e1 ? e0 : e1;
+    start = std::min(dst->interval_start, src->interval_start);
+    if (end - start > ~0ull) {
+      p3g::set_error("batch_aggregation_merge: interval overflow");
+      return PRIO3GPU_E_ARG;
+    }
+    dur = (uint64_t)(end - start);
+  }
+  // Aggregatable::merge: elementwise mod-p addition of canonical LE field elements
+  if (dst->aggregate_share) {
+    const u128 p = field_size == 16 ? (((u128)0xFFFFFFFFFFFFFFE4ull << 64) | 1u)
+                                    : (u128)0xFFFFFFFF00000001ull;
+    for (size_t e = 0; e < output_len; ++e) {
+      uint8_t* d = dst->aggregate_share + e * field_size;
+      const uint8_t* s = src->aggregate_share + e * field_size;
+      u128 a = 0, b = 0;
+      for (int i = (int)field_size - 1; i >= 0; --i) {
+        a = (a << 8) | d[i];
+        b = (b << 8) | s[i];
+      }
+      if (a >= p || b >= p) {
+        p3g::set_error("batch_aggregation_merge: aggregate share element out of range");
+        return PRIO3GPU_E_ARG;
+      }
+      u128 r = a + b;
+      if (r < a || r >= p) r -= p;  // a, b < p < 2^128: one subtraction, wrap-around included
+      for (uint32_t i = 0; i < field_size; ++i) d[i] = (uint8_t)(r >> (8 * i));
+    }
+  }
+  dst->report_count += src->report_count;
+  for (int i = 0; i < 32; ++i) dst->checksum[i] ^= src->checksum[i];
+  dst->interval_start = start;
+  dst->interval_duration = dur;
+  return 0;
+}
+
 int prio3gpu_apply_faults(size_t n, const uint8_t* faults, uint8_t* status) {
   if (n && (!faults || !status)) return PRIO3GPU_E_ARG;
   for (size_t i = 0; i < n; ++i)

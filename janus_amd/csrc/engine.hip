@@ -132,15 +132,22 @@ struct DevBuf {
   uint8_t* u8() const { return static_cast<uint8_t*>(p); }
 };
 
+// One id per kernel, named exactly as rocprofv3 reports it (kernel-trace names are the
+// template-stripped function names), so the bench's HIP-event table and the profiles agree.
 enum KernelId {
-  KID_QUERY = 0, KID_EXPAND, KID_JR, KID_FLP, KID_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_MERGE,
-  KID_OUT, KID_MERGE, KID_SHARD, KID_PROVE, KID_FLP_WIRES, KID_ACC_SPEC, KID_FPV_FINAL,
+  KID_QUERY = 0, KID_EXPAND, KID_HELPER_XOF, KID_JR, KID_FLP_WEIGHTS, KID_FLP_QUERY,
+  KID_FLP_WIRES, KID_FPV_WEIGHTS, KID_FPV_WIRES0, KID_FPV_WIRES1, KID_FPV_FINAL, KID_DECIDE,
+  KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
+  KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
+  KID_REPORT_META_FOLD,
   KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
-    "k_query_rand", "k_expand", "k_jr", "k_flp_query", "k_decide", "k_prepare_next",
-    "k_accum_partial", "k_accum_merge", "k_out_shares", "k_merge", "k_shard_*", "k_flp_prove",
-    "k_flp_wires", "k_accum_spec", "k_fpv_finalize"};
+    "k_query_rand", "k_expand", "k_helper_xof", "k_jr", "k_flp_weights", "k_flp_query",
+    "k_flp_wires", "k_fpv_weights", "k_fpv_wires0", "k_fpv_wires1", "k_fpv_finalize", "k_decide",
+    "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
+    "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
+    "k_shard_proof", "k_report_meta", "k_report_meta_fold"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -503,15 +510,18 @@ int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, 
   HIPCHK(hipMemsetAsync(flags, 0, n * 4, c->stream));
   const size_t lds = (size_t)16 * (3 * (size_t)g.m + g.chunk + 1 + 12) + 16;
   {
-    PROF(KID_FLP);
+    PROF(KID_FPV_WEIGHTS);
     hipLaunchKernelGGL(k_fpv_weights, dim3(N, 2), dim3(256), lds, c->stream, g, N, proof,
                        CRows{st->t.u8(), 32}, CRows{st->jr.u8(), 32}, prep, d_status, wrows, flags);
   }
   {
-    PROF(KID_FLP_WIRES);
+    PROF(KID_FPV_WIRES0);
     hipLaunchKernelGGL(k_fpv_wires0, dim3((g.chunk + 255) / 256, H, N), dim3(256), 0, c->stream, g,
                        N, H, meas, CRows{wrows.base, wrows.stride}, d_status, st->fpart.u8(),
                        flags);
+  }
+  {
+    PROF(KID_FPV_WIRES1);
     hipLaunchKernelGGL(k_fpv_wires1, dim3((g.chunk1 + 255) / 256, N), dim3(256), 0, c->stream, g, N,
                        meas, CRows{wrows.base, wrows.stride}, prep, d_status);
   }
@@ -559,7 +569,7 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
         uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
         HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
         {
-          PROF(KID_EXPAND);
+          PROF(KID_HELPER_XOF);
           hipLaunchKernelGGL(k_helper_xof, dim3((N + kHxRows - 1) / kHxRows), dim3(2 * kHxRows), 0,
                              c->stream, g, N,
                              CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
@@ -661,13 +671,13 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
   Rows wrows{nullptr, 0};
   if (psum) wrows = Rows{st->w.u8(), (size_t)flp_w_len(g) * es};
   if (psum && g.m <= 128 && g.chunk <= 128) {
-    PROF(KID_FLP);
+    PROF(KID_FLP_WEIGHTS);
     hipLaunchKernelGGL(k_flp_weights<FO>, grid1(n, 4), dim3(256), 0, c->stream, g, N, proof,
                        CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                        CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
                        wrows);
   } else {
-    PROF(KID_FLP);
+    PROF(KID_FLP_QUERY);
     hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr1), lds, c->stream, g, N, d1, meas, proof,
                        CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                        CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
@@ -692,7 +702,7 @@ int launch_decide(prio3gpu_ctx* c, size_t n, const uint8_t* d_l, const uint8_t* 
                   uint8_t* d_msg, uint8_t* d_status) {
   const Cfg& g = c->cfg;
   if (g.kind == KIND_FPVEC) {
-    PROF(KID_DECIDE);
+    PROF(KID_FPV_DECIDE);
     hipLaunchKernelGGL(k_fpv_decide, dim3((unsigned)n), dim3(256), 0, c->stream, g, (uint32_t)n,
                        CRows{d_l, g.prep_share_len}, CRows{d_h, g.prep_share_len},
                        Rows{d_msg, g.prep_msg_len}, d_status);
@@ -871,6 +881,27 @@ int launch_out_shares(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8
 
 bool is_f64(const prio3gpu_ctx* c) { return c->cfg.es == 8; }
 
+// Device slot meta (SHA-256 state words, [tmin, tmax]) <-> host BatchAggregation fields.
+prio3gpu_batch_aggregation slot_meta_to_ba(const SlotMeta& m) {
+  prio3gpu_batch_aggregation b{};
+  for (int i = 0; i < 8; ++i)
+    for (int k = 0; k < 4; ++k) b.checksum[4 * i + k] = (uint8_t)(m.ck[i] >> (24 - 8 * k));
+  if (m.tmin <= m.tmax) {
+    b.interval_start = m.tmin;
+    b.interval_duration = m.tmax - m.tmin + 1;
+  }
+  return b;
+}
+SlotMeta ba_to_slot_meta(const prio3gpu_batch_aggregation& b) {
+  SlotMeta m{};
+  for (int i = 0; i < 8; ++i)
+    m.ck[i] = ((uint32_t)b.checksum[4 * i] << 24) | ((uint32_t)b.checksum[4 * i + 1] << 16) |
+              ((uint32_t)b.checksum[4 * i + 2] << 8) | b.checksum[4 * i + 3];
+  m.tmin = b.interval_duration ? b.interval_start : ~0ull;
+  m.tmax = b.interval_duration ? b.interval_start + b.interval_duration - 1 : 0ull;
+  return m;
+}
+
 int check_state(prio3gpu_ctx* c, prio3gpu_state* st, size_t n) {
   if (!c || !st || st->ctx != c) {
     set_err("bad context/state");
@@ -924,6 +955,11 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
     if (v >= 64 && v <= 1024) c->wires_slots = (uint32_t)v;
   }
   if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
+  // Test switch: every XOF squeeze takes the exact per-element rejection path (the fast path's
+  // bulk stores are skipped), and the FixedPoint helper runs its exact two-pass XOF.
+  const char* ex = getenv("PRIO3GPU_EXACT_SQUEEZE");
+  const bool exact_squeeze = ex && ex[0] == '1';
+  if (exact_squeeze) c->fused_helper = false;
   c->device = device;
   memcpy(c->vk, verify_key, 16);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -937,6 +973,7 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
     prio3gpu_ctx_destroy(c);
     return rc;
   }
+  c->cfg.exact_squeeze = exact_squeeze ? 1u : 0u;
   *out = c;
   return 0;
 }
@@ -1150,14 +1187,20 @@ int prio3gpu_agg_update_reports(prio3gpu_agg* a, size_t n, const uint8_t* report
   if (batch_slots) CHK(stage_in(c, c->io[3], batch_slots, n * 4, &d_slots));
   const uint32_t nwaves = (uint32_t)((n + 255) / 256 * 4);
   CHK(a->wmeta.ensure((size_t)nwaves * sizeof(WaveMeta)));
-  hipLaunchKernelGGL(k_report_meta, grid1(n, 256), dim3(256), 0, c->stream, (uint32_t)n,
-                     CRows{d_ids, 16}, reinterpret_cast<const uint64_t*>(d_times), d_st,
-                     reinterpret_cast<const uint32_t*>(d_slots), a->slots,
-                     reinterpret_cast<SlotMeta*>(a->meta.p),
-                     reinterpret_cast<WaveMeta*>(a->wmeta.p));
-  hipLaunchKernelGGL(k_report_meta_fold, dim3(a->slots), dim3(256), 0, c->stream, nwaves,
-                     reinterpret_cast<const WaveMeta*>(a->wmeta.p),
-                     reinterpret_cast<SlotMeta*>(a->meta.p));
+  {
+    PROF(KID_REPORT_META);
+    hipLaunchKernelGGL(k_report_meta, grid1(n, 256), dim3(256), 0, c->stream, (uint32_t)n,
+                       CRows{d_ids, 16}, reinterpret_cast<const uint64_t*>(d_times), d_st,
+                       reinterpret_cast<const uint32_t*>(d_slots), a->slots,
+                       reinterpret_cast<SlotMeta*>(a->meta.p),
+                       reinterpret_cast<WaveMeta*>(a->wmeta.p));
+  }
+  {
+    PROF(KID_REPORT_META_FOLD);
+    hipLaunchKernelGGL(k_report_meta_fold, dim3(a->slots), dim3(256), 0, c->stream, nwaves,
+                       reinterpret_cast<const WaveMeta*>(a->wmeta.p),
+                       reinterpret_cast<SlotMeta*>(a->meta.p));
+  }
   HIPCHK(hipGetLastError());
   if (!is_device_ptr(report_ids) || !is_device_ptr(times)) HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
@@ -1410,7 +1453,7 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
   uint8_t* d_jr = d_prand + n * (size_t)std::max<uint32_t>(g.prove_rand_len, 1) * es;
   Rows helper{d_helper, g.helper_share_len}, leader{d_leader, g.leader_share_len};
   {
-    PROF(KID_SHARD);
+    PROF(KID_SHARD_SEEDS);
     hipLaunchKernelGGL(k_shard_seeds, grid1(n, 256), dim3(256), 0, c->stream, g, N,
                        CRows{d_rand, rs}, helper, leader);
   }
@@ -1421,9 +1464,12 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
                        CRows{d_helper, g.helper_share_len}, hm, hp, (const uint8_t*)nullptr);
   }
   {
-    PROF(KID_SHARD);
+    PROF(KID_SHARD_MEAS);
     hipLaunchKernelGGL(k_shard_meas<FO>, dim3((g.meas_len + 255) / 256, N), dim3(256), 0,
                        c->stream, g, N, d_meas, mw, CRows{hm.base, hm.stride}, leader);
+  }
+  {
+    PROF(KID_SHARD_JR);
     hipLaunchKernelGGL(k_shard_jr<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N,
                        CRows{d_nonces, 16}, CRows{d_rand, rs}, CRows{hm.base, hm.stride},
                        CRows{d_leader, g.leader_share_len}, Rows{d_pub, g.public_share_len},
@@ -1443,7 +1489,7 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
                        CRows{d_jr, 32}, Rows{d_proof, (size_t)g.proof_len * es});
   }
   {
-    PROF(KID_SHARD);
+    PROF(KID_SHARD_PROOF);
     hipLaunchKernelGGL(k_shard_proof<FO>, dim3((g.proof_len + 255) / 256, N), dim3(256), 0,
                        c->stream, g, N, CRows{d_proof, (size_t)g.proof_len * es},
                        CRows{hp.base, hp.stride}, leader);
@@ -1597,18 +1643,16 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
   std::vector<SlotMeta> mg((size_t)local->slots * cm->nranks), md(local->slots);
   HIPCHK(hipMemcpy(mg.data(), cm->mgather.p, mbytes * cm->nranks, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(md.data(), dst->meta.p, mbytes, hipMemcpyDeviceToHost));
+  // checksum XOR + interval union in rank order: BatchAggregation::merged_with's host half
+  // (prio3gpu_batch_aggregation_merge; the shares were merged on the GPU above, counts by RCCL)
   for (uint32_t s = 0; s < local->slots; ++s) {
-    if (!total) {
-      memset(md[s].ck, 0, sizeof md[s].ck);
-      md[s].tmin = ~0ull;
-      md[s].tmax = 0ull;
-    }
+    prio3gpu_batch_aggregation acc = total ? slot_meta_to_ba(md[s]) : slot_meta_to_ba(SlotMeta{
+                                                                          {0}, ~0ull, 0ull});
     for (int r = 0; r < cm->nranks; ++r) {
-      const SlotMeta& x = mg[(size_t)r * local->slots + s];
-      for (int i = 0; i < 8; ++i) md[s].ck[i] ^= x.ck[i];
-      md[s].tmin = std::min(md[s].tmin, x.tmin);
-      md[s].tmax = std::max(md[s].tmax, x.tmax);
+      const prio3gpu_batch_aggregation x = slot_meta_to_ba(mg[(size_t)r * local->slots + s]);
+      CHK(prio3gpu_batch_aggregation_merge(c->cfg.es, 0, &acc, &x));
     }
+    md[s] = ba_to_slot_meta(acc);
   }
   HIPCHK(hipMemcpyAsync(dst->meta.p, md.data(), mbytes, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(dst->counts.p, cur.data(), local->slots * 8, hipMemcpyHostToDevice,
@@ -1627,6 +1671,80 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
   }
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
+}
+
+}  // extern "C"
+
+namespace {
+// Test-only: the XOF squeeze (SqueezeVec, the code every XOF kernel runs) over caller-crafted rate
+// blocks -- blocks[25 i .. 25 i + 25) is the state after the i-th "permutation" -- so the exact
+// rejection branches (non-canonical elements, the element straddling two Field128 blocks) run on
+// inputs that real SHAKE128 output reaches with probability 28 / 2^64 per element.  One lane.
+template <class FO>
+__global__ void k_test_squeeze(const uint64_t* blocks, uint32_t nblocks, uint32_t n, uint8_t* out,
+                               uint32_t exact, uint32_t* overrun) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t s[25];
+  for (int i = 0; i < 25; ++i) s[i] = blocks[i];
+  uint32_t b = 0;
+  SqueezeVec<FO>::run(s, n, out, exact != 0u, [&](uint64_t st[25]) {
+    ++b;
+    const bool have = b < nblocks;
+    for (int i = 0; i < 25; ++i) st[i] = have ? blocks[25 * (size_t)b + i] : 0ull;
+    if (!have) *overrun = 1u;
+  });
+}
+}  // namespace
+
+extern "C" {
+
+int prio3gpu_test_squeeze(int field_size, const uint64_t* blocks, size_t nblocks, uint32_t n,
+                          uint8_t* out, int exact) {
+  if ((field_size != 8 && field_size != 16) || !blocks || nblocks == 0 || (n && !out)) {
+    set_err("test_squeeze: bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  if (n == 0) return 0;
+  void *d_blocks = nullptr, *d_out = nullptr, *d_over = nullptr;
+  const size_t bb = nblocks * 25 * 8, ob = (size_t)n * field_size;
+  int rc = 0;
+  uint32_t over = 0;
+  if (hipMalloc(&d_blocks, bb) != hipSuccess || hipMalloc(&d_out, ob) != hipSuccess ||
+      hipMalloc(&d_over, 4) != hipSuccess) {
+    set_err("test_squeeze: hipMalloc failed");
+    rc = PRIO3GPU_E_HIP;
+  }
+  if (!rc && (hipMemcpy(d_blocks, blocks, bb, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemset(d_over, 0, 4) != hipSuccess || hipMemset(d_out, 0, ob) != hipSuccess)) {
+    set_err("test_squeeze: copy failed");
+    rc = PRIO3GPU_E_HIP;
+  }
+  if (!rc) {
+    if (field_size == 16)
+      hipLaunchKernelGGL(k_test_squeeze<Field128Ops>, dim3(1), dim3(64), 0, nullptr,
+                         static_cast<const uint64_t*>(d_blocks), (uint32_t)nblocks, n,
+                         static_cast<uint8_t*>(d_out), (uint32_t)(exact != 0),
+                         static_cast<uint32_t*>(d_over));
+    else
+      hipLaunchKernelGGL(k_test_squeeze<Field64Ops>, dim3(1), dim3(64), 0, nullptr,
+                         static_cast<const uint64_t*>(d_blocks), (uint32_t)nblocks, n,
+                         static_cast<uint8_t*>(d_out), (uint32_t)(exact != 0),
+                         static_cast<uint32_t*>(d_over));
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, d_out, ob, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&over, d_over, 4, hipMemcpyDeviceToHost) != hipSuccess) {
+      set_err("test_squeeze: kernel failed");
+      rc = PRIO3GPU_E_HIP;
+    }
+  }
+  if (!rc && over) {
+    set_err("test_squeeze: the squeeze needed more blocks than supplied");
+    rc = PRIO3GPU_E_ARG;
+  }
+  if (d_blocks) (void)hipFree(d_blocks);
+  if (d_out) (void)hipFree(d_out);
+  if (d_over) (void)hipFree(d_over);
+  return rc;
 }
 
 int prio3gpu_prof_enable(prio3gpu_ctx* c, int on) {

@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
     if (live) {
       if (bad) atomicAdd(fallback, 1u);
       xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), 1u,
-                                 cfg.proof_len, out_proof.at(r));
+                                 cfg.proof_len, out_proof.at(r), cfg.exact_squeeze);
     }
     return;
   }
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
   m.pad(25);
   uint64_t s2[25];
   sponge_one_block<24>(s2, m);
-  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r));
+  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r), cfg.exact_squeeze);
 }
 
 // Per-report weight row ("W"), element offsets (Field128 elements).

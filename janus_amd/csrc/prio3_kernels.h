@@ -51,6 +51,7 @@ struct Cfg {
   uint32_t bits, length, chunk, calls, m, logm, arity, gp_len;
   uint32_t leader_share_len, helper_share_len, public_share_len, prep_share_len, prep_msg_len;
   uint32_t qr_len;          // query-randomness elements (one per gadget)
+  uint32_t exact_squeeze;   // test switch: every XOF squeeze takes the per-element path
   const uint8_t* twiddles;  // device: alpha_m^k, k < m, Montgomery form, ES bytes each
   // FixedPointBoundedL2VecSum's second gadget, ParallelSum(PolyEval(norm poly), chunk1)
   uint32_t chunk1, calls1, m1, logm1, gp_len1;
@@ -75,9 +76,12 @@ DEVI void st64(uint8_t* p, uint64_t v) { *reinterpret_cast<uint64_t*>(p) = v; }
 // ------------------------------------------------------------------------------------------------
 // Squeeze n field elements (prio `into_field_vec`: ES-byte LE chunks, reject >= p) from a state
 // that has just been permuted after absorbing.  Accepted element i goes to out + i*ES.
+// `next(s)` produces the next rate block (keccak_p<24> for the XOF; the test kernel
+// k_test_squeeze feeds caller-crafted blocks instead).  `exact` forces the per-element
+// rejection-sampling path for every block (PRIO3GPU_EXACT_SQUEEZE=1, a test switch).
 // ------------------------------------------------------------------------------------------------
-template <class FO, int NR>
-DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out);
+template <class FO>
+struct SqueezeVec;
 
 // One permutation per loop iteration (a single inlined Keccak-f per loop: ~35 KB of VOP3 code, so
 // two hot copies would not fit the instruction cache).  168-byte blocks alternate parity: even
@@ -89,91 +93,108 @@ DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out);
 DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 
 template <>
-DEVI void squeeze_vec<Field128Ops, 24>(uint64_t s[25], uint32_t n, uint8_t* out) {
-  using FO = Field128Ops;
-  uint32_t cnt = 0;
-  uint32_t parity = 0;
-  uint64_t carry = 0;
-  while (true) {
-    bool fast = cnt + 11u <= n;
-    if (parity == 0) {
-#pragma unroll
-      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 1]);
-    } else {
-      fast &= hi_ok(s[0]);
-#pragma unroll
-      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
-    }
-    if (fast) {
-      uint64_t* o = reinterpret_cast<uint64_t*>(out + (size_t)cnt * 16);
+struct SqueezeVec<Field128Ops> {
+  template <class Next>
+  static DEVI void run(uint64_t s[25], uint32_t n, uint8_t* out, bool exact, Next next) {
+    using FO = Field128Ops;
+    uint32_t cnt = 0;
+    uint32_t parity = 0;
+    uint64_t carry = 0;
+    while (true) {
+      bool fast = !exact && cnt + 11u <= n;
       if (parity == 0) {
 #pragma unroll
-        for (int k = 0; k < 10; ++k)
-          *reinterpret_cast<ulonglong2*>(o + 2 * k) = make_ulonglong2(s[2 * k], s[2 * k + 1]);
-        carry = s[20];
-        cnt += 10u;
+        for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 1]);
       } else {
-        *reinterpret_cast<ulonglong2*>(o) = make_ulonglong2(carry, s[0]);
+        fast &= hi_ok(s[0]);
 #pragma unroll
-        for (int k = 0; k < 10; ++k)
-          *reinterpret_cast<ulonglong2*>(o + 2 * k + 2) = make_ulonglong2(s[2 * k + 1], s[2 * k + 2]);
-        cnt += 11u;
+        for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
       }
-    } else if (parity == 0) {
+      if (fast) {
+        uint64_t* o = reinterpret_cast<uint64_t*>(out + (size_t)cnt * 16);
+        if (parity == 0) {
 #pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
-        if (cnt < n && FO::is_canonical(e)) {
-          FO::store(out + (size_t)cnt * 16, e);
-          ++cnt;
+          for (int k = 0; k < 10; ++k)
+            *reinterpret_cast<ulonglong2*>(o + 2 * k) = make_ulonglong2(s[2 * k], s[2 * k + 1]);
+          carry = s[20];
+          cnt += 10u;
+        } else {
+          *reinterpret_cast<ulonglong2*>(o) = make_ulonglong2(carry, s[0]);
+#pragma unroll
+          for (int k = 0; k < 10; ++k)
+            *reinterpret_cast<ulonglong2*>(o + 2 * k + 2) = make_ulonglong2(s[2 * k + 1], s[2 * k + 2]);
+          cnt += 11u;
+        }
+      } else if (parity == 0) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
+          if (cnt < n && FO::is_canonical(e)) {
+            FO::store(out + (size_t)cnt * 16, e);
+            ++cnt;
+          }
+        }
+        carry = s[20];
+      } else {
+        {
+          F128 e = FO::from_u64x2(carry, s[0]);
+          if (cnt < n && FO::is_canonical(e)) {
+            FO::store(out + (size_t)cnt * 16, e);
+            ++cnt;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+          F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
+          if (cnt < n && FO::is_canonical(e)) {
+            FO::store(out + (size_t)cnt * 16, e);
+            ++cnt;
+          }
         }
       }
-      carry = s[20];
-    } else {
-      {
-        F128 e = FO::from_u64x2(carry, s[0]);
-        if (cnt < n && FO::is_canonical(e)) {
-          FO::store(out + (size_t)cnt * 16, e);
-          ++cnt;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
-        if (cnt < n && FO::is_canonical(e)) {
-          FO::store(out + (size_t)cnt * 16, e);
-          ++cnt;
-        }
-      }
+      if (cnt >= n) break;
+      parity ^= 1u;
+      next(s);
     }
-    if (cnt >= n) break;
-    parity ^= 1u;
-    keccak_p<24>(s);
   }
-}
+};
 
+// Field64: 21 whole elements per block, always the per-element path.
 template <>
-DEVI void squeeze_vec<Field64Ops, 24>(uint64_t s[25], uint32_t n, uint8_t* out) {
-  using FO = Field64Ops;
-  uint32_t cnt = 0;
-  while (true) {
+struct SqueezeVec<Field64Ops> {
+  template <class Next>
+  static DEVI void run(uint64_t s[25], uint32_t n, uint8_t* out, bool /*exact*/, Next next) {
+    using FO = Field64Ops;
+    uint32_t cnt = 0;
+    while (true) {
 #pragma unroll
-    for (int k = 0; k < 21; ++k) {
-      if (cnt < n && s[k] < FO::P) {
-        st64(out + (size_t)cnt * 8, s[k]);
-        ++cnt;
+      for (int k = 0; k < 21; ++k) {
+        if (cnt < n && s[k] < FO::P) {
+          st64(out + (size_t)cnt * 8, s[k]);
+          ++cnt;
+        }
       }
+      if (cnt >= n) break;
+      next(s);
     }
-    if (cnt >= n) break;
-    keccak_p<24>(s);
   }
+};
+
+struct KeccakNext {
+  DEVI void operator()(uint64_t s[25]) const { keccak_p<24>(s); }
+};
+
+template <class FO, int NR>
+DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out, bool exact = false) {
+  static_assert(NR == 24, "XofShake128");
+  SqueezeVec<FO>::run(s, n, out, exact, KeccakNext{});
 }
 
 // XOF(seed, dst(usage), binder=[byte]) expanded into n elements (helper share expansion).
 template <class FO>
 DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed_lo,
                                  uint64_t seed_hi, uint32_t binder_byte, uint32_t n,
-                                 uint8_t* out) {
+                                 uint8_t* out, bool exact) {
   MsgBlock m;
   m.clear();
   m.header(algo_id, usage, seed_lo, seed_hi);
@@ -181,7 +202,7 @@ DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed
   m.pad(26);
   uint64_t s[25];
   sponge_one_block<24>(s, m);
-  squeeze_vec<FO, 24>(s, n, out);
+  squeeze_vec<FO, 24>(s, n, out, exact);
 }
 
 // derive_seed(0^16, dst6, part0 || part1)   (prio Prio3::derive_joint_rand_seed)
@@ -291,7 +312,7 @@ __global__ void __launch_bounds__(256) k_query_rand(Cfg cfg, uint32_t n, uint64_
   m.pad(41);
   uint64_t s[25];
   sponge_one_block<24>(s, m);
-  squeeze_vec<FO, 24>(s, cfg.qr_len, out_t.at(r));
+  squeeze_vec<FO, 24>(s, cfg.qr_len, out_t.at(r), cfg.exact_squeeze);
 }
 
 // Helper share expansion: meas share XOF(k_meas, dst1, [agg_id]) and proof share
@@ -305,9 +326,9 @@ __global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t ag
   if (status && status[r] != ST_OK) return;
   const uint8_t* hs = helper_shares.at(r);
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), agg_id,
-                             cfg.proof_len, out_proof.at(r));
+                             cfg.proof_len, out_proof.at(r), cfg.exact_squeeze);
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8), agg_id,
-                             cfg.meas_len, out_meas.at(r));
+                             cfg.meas_len, out_meas.at(r), cfg.exact_squeeze);
 }
 
 // Joint randomness (prio prepare_init): own part over the encoded meas share, corrected seed
@@ -489,7 +510,7 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
   m.pad(25);
   uint64_t s2[25];
   sponge_one_block<24>(s2, m);
-  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r));
+  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r), cfg.exact_squeeze);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1842,7 +1863,7 @@ __global__ void __launch_bounds__(256) k_shard_jr(Cfg cfg, uint32_t n, CRows non
     mb.pad(25);
     uint64_t s[25];
     sponge_one_block<24>(s, mb);
-    squeeze_vec<FO, 24>(s, cfg.jr_len, jr_out.at(r));
+    squeeze_vec<FO, 24>(s, cfg.jr_len, jr_out.at(r), cfg.exact_squeeze);
   }
   MsgBlock mb;
   mb.clear();
@@ -1850,7 +1871,7 @@ __global__ void __launch_bounds__(256) k_shard_jr(Cfg cfg, uint32_t n, CRows non
   mb.pad(25);
   uint64_t s[25];
   sponge_one_block<24>(s, mb);
-  squeeze_vec<FO, 24>(s, cfg.prove_rand_len, prove_rand_out.at(r));
+  squeeze_vec<FO, 24>(s, cfg.prove_rand_len, prove_rand_out.at(r), cfg.exact_squeeze);
 }
 
 // leader proof share = proof - helper proof share   (thread per element)

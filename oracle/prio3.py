@@ -107,21 +107,27 @@ class XofShake128:
         return hashlib.shake_128(self.msg).digest(n)
 
     def next_vec(self, fld, length: int) -> List[int]:
-        """prio `into_field_vec`: read ENCODED_SIZE-byte LE chunks, reject values >= p
-        (the mask is all-ones for Field64/Field128, so masking is a no-op)."""
-        es = fld.ENCODED_SIZE
-        nbytes = es * length + 64
+        """prio `into_field_vec` over the XOF stream (see field_vec_from_stream)."""
+        nbytes = fld.ENCODED_SIZE * length + 64
         while True:
-            buf = self.stream(nbytes)
-            out, off = [], 0
-            while len(out) < length and off + es <= len(buf):
-                x = int.from_bytes(buf[off:off + es], "little")
-                off += es
-                if x < fld.MODULUS:
-                    out.append(x)
-            if len(out) == length:
+            out = field_vec_from_stream(fld, self.stream(nbytes), length)
+            if out is not None:
                 return out
             nbytes *= 2
+
+
+def field_vec_from_stream(fld, buf: bytes, length: int) -> Optional[List[int]]:
+    """prio 0.15.1 `into_field_vec` (src/field.rs, via XofShake128::next_vec): read
+    ENCODED_SIZE-byte LE chunks of the stream in order and keep those < p (rejection sampling; the
+    mask is all-ones for Field64/Field128, so masking is a no-op).  None if `buf` runs out first."""
+    es = fld.ENCODED_SIZE
+    out, off = [], 0
+    while len(out) < length and off + es <= len(buf):
+        x = int.from_bytes(buf[off:off + es], "little")
+        off += es
+        if x < fld.MODULUS:
+            out.append(x)
+    return out if len(out) == length else None
 
 
 def derive_seed(seed: bytes, dst: bytes, binder: bytes) -> bytes:

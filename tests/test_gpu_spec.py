@@ -51,6 +51,53 @@ def _plain(name, meas, sel):
     return int(m[:, 0].sum())
 
 
+def test_sumvec_8_1000_multichunk_fold_bytes_vs_c_restatement():
+    """The headline config at a size that reaches the multi-chunk speculative fold (WCH = 32 waves
+    = 2,048 reports per chunk, engine.hip launch_accumulate): 4,200 SumVec(8, 1000) reports,
+    slot 0 over 36 whole waves (two speculative chunks), slot 1 over 28 waves, one mixed-slot wave
+    (direct path) and a partial last wave of 40 rows on slot 2; six reports tampered inside the
+    column-summed window (element 500) so k_accum_spec must subtract their rows.  Both
+    aggregators' aggregate shares and counts per slot must equal the C restatement's bytes."""
+    from janus_amd.prio3 import Prio3Gpu
+    from oracle import prio3 as O
+    from oracle.ref import Prio3Ref
+    n = 4200
+    vk = O.synth_verify_key(b"spec-fold")
+    ref = Prio3Ref(2, vk, 8, 1000, 89)
+    g = ref.gen(b"spec-fold", 0, n, threads=16)
+    lin = g["leader_in"].copy()
+    bad = [5, 70, 2100, 3000, 4130, 4199]
+    for r in bad:
+        off = 500 * 16
+        x = (int.from_bytes(lin[r, off:off + 16].tobytes(), "little") + 1) % O.Field128.MODULUS
+        lin[r, off:off + 16] = np.frombuffer(x.to_bytes(16, "little"), np.uint8)
+    slots = np.zeros(n, np.uint32)
+    slots[2304:4096] = 1
+    slots[4096:4160] = np.random.default_rng(3).integers(0, 3, 64)
+    slots[4160:] = 2
+    v = Prio3Gpu.new_sum_vec(8, 1000, 89, vk)
+    ls, hs = v.new_state(0, n), v.new_state(1, n)
+    lp, lst = v.prepare_init(ls, g["nonces"], g["public"], lin)
+    hagg, lagg = v.new_aggregate(3), v.new_aggregate(3)
+    msgs, hst = v.helper_init(hs, g["nonces"], g["public"], g["helper_in"], lp, agg=hagg,
+                              batch_slots=slots)
+    _, lst = v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg, batch_slots=slots)
+    ok = np.ones(n, bool)
+    ok[bad] = False
+    assert (hst[bad] == 5).all() and (hst[ok] == 0).all() and (lst == hst).all()
+    for q in range(3):
+        sel = np.nonzero(slots == q)[0]
+        res = ref.prepare_batch(np.ascontiguousarray(g["nonces"][sel]),
+                                np.ascontiguousarray(g["public"][sel]),
+                                np.ascontiguousarray(lin[sel]),
+                                np.ascontiguousarray(g["helper_in"][sel]), threads=16,
+                                outputs=False)
+        (la, lc), (ha, hc) = lagg.read(q), hagg.read(q)
+        assert lc == hc == res["count"] == int(ok[sel].sum())
+        assert la == res["agg_l"].tobytes(), f"leader slot {q}"
+        assert ha == res["agg_h"].tobytes(), f"helper slot {q}"
+
+
 @pytest.mark.parametrize("name", ["hist256", "sumvec_small", "sum32", "countvec15"])
 def test_speculative_matches_direct_and_plaintext(name):
     n = 300

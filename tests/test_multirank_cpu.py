@@ -1,8 +1,15 @@
-"""N > 1 path on CPU (gloo, world_size 2): reports sharded by janus_amd.parallel.shard_range, each
-rank aggregates its shard (C restatement as the stand-in for the GPU, which this container lacks),
-partial aggregate shares are all-gathered as raw LE bytes and merged mod p in rank order -- the
-exchange Comm.allreduce performs with RCCL on the GPU.  The merged result must equal the
-single-process aggregate over all reports, for both aggregators, bit for bit."""
+"""N > 1 path on CPU (gloo, world_size 2).  Reports are sharded by janus_amd.parallel.shard_range;
+each rank aggregates its shard (the C restatement stands in for the GPU, which this container
+lacks) into a `BatchAggregation` per aggregator (aggregate share, count, ReportIdChecksum,
+client-timestamp interval); the partials are all-gathered and folded in rank order by the
+product's merge, prio3gpu_batch_aggregation_merge (janus_amd.parallel.merge_batch_aggregations)
+-- the host half of the exchange Comm.allreduce performs after its RCCL all-gather.  The merged
+result must equal the single-process aggregation over all reports, bit for bit.
+
+Reference semantics: BatchAggregation::merged_with (aggregator_core/src/datastore/models.rs:
+962-991), Interval::merge (core/src/time.rs:289-302, test cases :357-406), ReportIdChecksum
+(core/src/report_id.rs:18-44), batch-aggregation shard merge (aggregate_share.rs:47-65)."""
+import hashlib
 import os
 import socket
 
@@ -12,6 +19,7 @@ import torch.multiprocessing as mp
 
 N = 24
 NAME = "hist4"
+T0 = 1_600_000_000
 
 
 def _free_port():
@@ -22,59 +30,99 @@ def _free_port():
     return p
 
 
+def _checksum(nonces):
+    ck = np.zeros(32, np.uint8)
+    for r in range(len(nonces)):
+        ck ^= np.frombuffer(hashlib.sha256(nonces[r].tobytes()).digest(), np.uint8)
+    return ck.tobytes()
+
+
+def _times(lo, hi):
+    return [T0 + 37 * i + (i % 5) for i in range(lo, hi)]
+
+
+def _partials(lo, hi):
+    """(leader, helper) BatchAggregations of reports [lo, hi) from the C restatement."""
+    from janus_amd.parallel import BatchAggregation
+    from oracle import prio3 as O
+    from oracle.ref import Prio3Ref
+    from tests.reports import CONFIGS
+    c = CONFIGS[NAME]
+    r = Prio3Ref(c["kind"], O.synth_verify_key(b"mr"), c["bits"], c["length"], c["chunk"])
+    g = r.gen(b"mr", lo, hi - lo, threads=1)
+    res = r.prepare_batch(g["nonces"], g["public"], g["leader_in"], g["helper_in"], threads=1,
+                          outputs=False)
+    ck = _checksum(g["nonces"])
+    t = _times(lo, hi)
+    iv = (min(t), max(t) - min(t) + 1) if t else (0, 0)
+    return tuple(BatchAggregation(res[k].tobytes(), res["count"], ck, iv)
+                 for k in ("agg_l", "agg_h"))
+
+
 def _rank_main(rank, world, port, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from janus_amd.parallel import shard_range
-    from oracle.ref import Prio3Ref
-    from tests.reports import CONFIGS
-    from oracle import prio3 as O
-    c = CONFIGS[NAME]
-    vk = O.synth_verify_key(b"mr")
-    r = Prio3Ref(c["kind"], vk, c["bits"], c["length"], c["chunk"])
+    from janus_amd.parallel import merge_batch_aggregations, shard_range
     lo, hi = shard_range(N, world, rank)
-    g = r.gen(b"mr", lo, hi - lo, threads=1)
-    res = r.prepare_batch(g["nonces"], g["public"], g["leader_in"], g["helper_in"], threads=1,
-                          outputs=False)
+    mine = _partials(lo, hi)
     parts = [None] * world
-    dist.all_gather_object(parts, (res["agg_l"].tobytes(), res["agg_h"].tobytes(), res["count"]))
-    p, es = O.Field128.MODULUS, 16
-    merged = []
-    for which in (0, 1):
-        acc = [0] * (len(parts[0][which]) // es)
-        for part in parts:  # rank order
-            vec = O.Field128.decode_vec(part[which])
-            acc = [(a + b) % p for a, b in zip(acc, vec)]
-        merged.append(O.Field128.encode_vec(acc))
-    count = sum(part[2] for part in parts)
-    if rank == 0:
-        q.put((merged[0], merged[1], count))
+    dist.all_gather_object(parts, mine)
+    merged = [merge_batch_aggregations(16, [p[which] for p in parts]) for which in (0, 1)]
+    q.put((rank, merged))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_two_rank_shard_and_merge():
-    from oracle.ref import Prio3Ref
-    from tests.reports import CONFIGS
-    from oracle import prio3 as O
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
     for p_ in procs:
         p_.start()
-    got = q.get(timeout=120)
+    got = dict(q.get(timeout=180) for _ in procs)
     for p_ in procs:
         p_.join(timeout=60)
         assert p_.exitcode == 0
-    c = CONFIGS[NAME]
-    r = Prio3Ref(c["kind"], O.synth_verify_key(b"mr"), c["bits"], c["length"], c["chunk"])
-    g = r.gen(b"mr", 0, N, threads=1)
-    res = r.prepare_batch(g["nonces"], g["public"], g["leader_in"], g["helper_in"], threads=1,
-                          outputs=False)
-    assert got[0] == res["agg_l"].tobytes() and got[1] == res["agg_h"].tobytes()
-    assert got[2] == N == res["count"]
+    want = _partials(0, N)  # one process over every report
+    for rank in (0, 1):  # every rank holds the same merged totals
+        for which in (0, 1):
+            g, w = got[rank][which], want[which]
+            assert g.aggregate_share == w.aggregate_share
+            assert g.report_count == w.report_count == N
+            assert g.checksum == w.checksum
+            assert g.interval == w.interval
+
+
+def test_merge_interval_reference_cases():
+    """Interval::merge as the reference's own test pins it (core/src/time.rs:357-406)."""
+    from janus_amd.parallel import BatchAggregation, merge_batch_aggregations
+    cases = [((0, 10), (20, 10), (0, 30)), ((0, 10), (5, 10), (0, 15)), ((0, 10), (2, 8), (0, 10)),
+             ((0, 10), (0, 10), (0, 10)), ((0, 0), (0, 10), (0, 10)), ((0, 10), (0, 0), (0, 10)),
+             ((0, 0), (0, 0), (0, 0))]
+    for lhs, rhs, want in cases:
+        a = BatchAggregation(bytes(16), 1, bytes(32), lhs)
+        b = BatchAggregation(bytes(16), 2, bytes(32), rhs)
+        m = merge_batch_aggregations(16, [a, b])
+        assert m.interval == want and m.report_count == 3
+
+
+def test_merge_mod_p_and_checksum():
+    from janus_amd.parallel import BatchAggregation, merge_batch_aggregations
+    from janus_amd.prio3 import FIELD64_MODULUS as P64, FIELD128_MODULUS as P128
+    from janus_amd._lib import Prio3GpuError
+    for es, p in ((16, P128), (8, P64)):
+        xs = [p - 1, p - 2, 5, 0]
+        ys = [p - 1, 3, p - 5, 0]
+        enc = lambda v: b"".join(int(x).to_bytes(es, "little") for x in v)
+        a = BatchAggregation(enc(xs), 1, bytes(range(32)), (5, 1))
+        b = BatchAggregation(enc(ys), 1, bytes(32 * [0xFF]), (9, 1))
+        m = merge_batch_aggregations(es, [a, b])
+        assert m.aggregate_share == enc([(x + y) % p for x, y in zip(xs, ys)])
+        assert m.checksum == bytes(i ^ 0xFF for i in range(32)) and m.interval == (5, 5)
+        with pytest.raises(Prio3GpuError):  # a non-canonical element is refused
+            merge_batch_aggregations(es, [a, BatchAggregation(enc([p, 0, 0, 0]), 1)])
 
 
 def test_shard_ranges_cover():
