@@ -139,7 +139,7 @@ enum KernelId {
   KID_FLP_WIRES, KID_FPV_WEIGHTS, KID_FPV_WIRES0, KID_FPV_WIRES1, KID_FPV_FINAL, KID_DECIDE,
   KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
   KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
-  KID_REPORT_META_FOLD,
+  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE,
   KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
@@ -147,7 +147,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_flp_wires", "k_fpv_weights", "k_fpv_wires0", "k_fpv_wires1", "k_fpv_finalize", "k_decide",
     "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
     "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
-    "k_shard_proof", "k_report_meta", "k_report_meta_fold"};
+    "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -185,6 +185,7 @@ struct prio3gpu_ctx {
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
   bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
   bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
+  bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
@@ -668,11 +669,19 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
     set_err("FLP LDS requirement %zu too large", lds);
     return PRIO3GPU_E_ARG;
   }
-  Rows wrows{nullptr, 0};
-  if (psum) wrows = Rows{st->w.u8(), (size_t)flp_w_len(g) * es};
-  if (psum && g.m <= 128 && g.chunk <= 128) {
+  // weight rows (row-major), then k_flp_weights' element-major scratch (calls x n entries)
+  WMat wrows{nullptr, 0, 0};
+  if (psum) wrows = WMat{st->w.u8(), (size_t)flp_w_len(g) * es, (size_t)es};
+  uint8_t* wscr = psum ? st->w.u8() + (size_t)N * flp_w_len(g) * es : nullptr;
+  if (psum && FO::ES == 16 && c->flp_weights_lane) {
     PROF(KID_FLP_WEIGHTS);
-    hipLaunchKernelGGL(k_flp_weights<FO>, grid1(n, 4), dim3(256), 0, c->stream, g, N, proof,
+    hipLaunchKernelGGL(k_flp_weights, grid1(n, kFwThreads), dim3(kFwThreads), 0, c->stream, g, N,
+                       proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
+                       wrows, wscr);
+  } else if (psum && g.m <= 128 && g.chunk <= 128) {
+    PROF(KID_FLP_WEIGHTS_WAVE);
+    hipLaunchKernelGGL(k_flp_weights_wave<FO>, grid1(n, 4), dim3(256), 0, c->stream, g, N, proof,
                        CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                        CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
                        wrows);
@@ -688,7 +697,7 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
     lds2 = (lds2 + 15) & ~(size_t)15;
     PROF(KID_FLP_WIRES);
     hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
-                       CRows{wrows.base, wrows.stride}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                       wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                        Rows{st->prep.u8(), g.prep_share_len}, d_status);
   }
   HIPCHK(hipGetLastError());
@@ -950,6 +959,7 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
   auto* c = new prio3gpu_ctx();
   if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
   if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) c->fused_helper = fh[0] != '0';
+  if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
     const long v = strtol(ws, nullptr, 10);
     if (v >= 64 && v <= 1024) c->wires_slots = (uint32_t)v;
@@ -1037,7 +1047,7 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   rc |= st->msg.ensure(N * 16);
   rc |= st->status.ensure(N);
   if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM)
-    rc |= st->w.ensure(N * (size_t)flp_w_len(g) * g.es);
+    rc |= st->w.ensure(N * (size_t)(flp_w_len(g) + g.calls) * g.es);  // rows + weights scratch
   if (g.kind == KIND_FPVEC) {
     rc |= st->w.ensure(N * (size_t)fpv_w_layout(g).len * 16);
     rc |= st->fpart.ensure(N * (size_t)fpv_rows(g) * g.chunk * 32);

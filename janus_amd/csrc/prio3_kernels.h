@@ -70,6 +70,14 @@ struct CRows {
   DEVI const uint8_t* at(size_t r) const { return base + r * stride; }
 };
 
+// FLP weight matrix (k_flp_weights* -> k_flp_wires): element e of report r at base + r rs + e es
+// (row-major: rs = row bytes, es = ES).
+struct WMat {
+  uint8_t* base;
+  size_t rs, es;
+  DEVI uint8_t* el(size_t r, uint32_t e) const { return base + r * rs + (size_t)e * es; }
+};
+
 DEVI uint64_t ld64(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
 DEVI void st64(uint8_t* p, uint64_t v) { *reinterpret_cast<uint64_t*>(p) = v; }
 
@@ -671,7 +679,7 @@ __host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.c
 template <class FO>
 __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
                                                    CRows proof, CRows tq, CRows jr, CRows part,
-                                                   Rows out_prep, uint8_t* status, Rows wrows) {
+                                                   Rows out_prep, uint8_t* status, WMat wm) {
   using T = typename FO::T;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t r = blockIdx.x;
@@ -764,13 +772,12 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
   T xsum = FO::zero();  // Histogram sum check
   uint8_t* outp = out_prep.at(r);
   const size_t ES = FO::ES;
-  if ((cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) && wrows.base != nullptr) {
+  if ((cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) && wm.base != nullptr) {
     // split mode: hand the weights to k_flp_wires (which streams the measurement share)
-    uint8_t* wr = wrows.at(r);
     const uint32_t C = cfg.calls;
     for (uint32_t k = tid; k < C; k += nthr) {
-      FO::store(wr + (size_t)k * ES, MM[k + 1]);
-      FO::store(wr + (size_t)(C + k) * ES, LM[k + 1]);
+      FO::store(wm.el(r, k), MM[k + 1]);
+      FO::store(wm.el(r, C + k), LM[k + 1]);
     }
     const T l0 = LM[0];
     const T half_l = FO::mul(lsum, FO::half());
@@ -778,14 +785,14 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
       const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
       const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
       bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
-      FO::store(wr + (size_t)(2 * C + j) * ES, RP[j + 1]);  // Montgomery
-      FO::store(wr + (size_t)(2 * C + c + j) * ES, FO::mul(l0, s0));
-      FO::store(wr + (size_t)(2 * C + 2 * c + j) * ES, FO::sub(FO::mul(l0, s1), half_l));
+      FO::store(wm.el(r, 2 * C + j), RP[j + 1]);  // Montgomery
+      FO::store(wm.el(r, 2 * C + c + j), FO::mul(l0, s0));
+      FO::store(wm.el(r, 2 * C + 2 * c + j), FO::sub(FO::mul(l0, s1), half_l));
     }
     if (bad) atomicOr(flag, 1u);
     __syncthreads();
     if (tid == 0) {
-      FO::store(wr + (size_t)(2 * C + 3 * c) * ES, gsum);
+      FO::store(wm.el(r, 2 * C + 3 * c), gsum);
       if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
       FO::store(outp + (size_t)(1 + arity) * ES, pt);
       const uint8_t* pp = part.at(r);
@@ -952,9 +959,9 @@ DEVI typename FO::T sel(bool c, const typename FO::T& a, const typename FO::T& b
 #define FLPW_WAVES __attribute__((amdgpu_waves_per_eu(6)))
 #endif
 template <class FO>
-__global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_t n, CRows proof, CRows tq,
+__global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights_wave(Cfg cfg, uint32_t n, CRows proof, CRows tq,
                                                      CRows jr, CRows part, Rows out_prep,
-                                                     uint8_t* status, Rows wrows) {
+                                                     uint8_t* status, WMat wm) {
   using T = typename FO::T;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1055,7 +1062,6 @@ __global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_
   T ql = shfl_T<FO>(qa, (int)((lane + 63u) & 63u));
   ql = sel<FO>(lane == 0, one, ql);  // rc^lane
   const T q64 = shfl_T<FO>(qa, 63);
-  uint8_t* wr = wrows.at(r);
 #pragma unroll
   for (uint32_t e = 0; e < 2; ++e) {
     const uint32_t p = 64u * e + lane;
@@ -1064,8 +1070,8 @@ __global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_
     if (e < E && p < m && k >= 1u && k <= C) {
       T mm = FO::mul(LMv[e], qk);
       if (k - 1u >= 64u) mm = FO::mul(mm, q64);
-      FO::store(wr + (size_t)(k - 1u) * ES, mm);
-      FO::store(wr + (size_t)(C + k - 1u) * ES, LMv[e]);
+      FO::store(wm.el(r, k - 1u), mm);
+      FO::store(wm.el(r, C + k - 1u), LMv[e]);
     }
   }
   const T half_l = FO::mul(lsum, FO::half());
@@ -1073,17 +1079,17 @@ __global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_
   for (uint32_t q = 0; q < 2; ++q) {
     const uint32_t j = lane + 64u * q;
     if (j < c) {
-      FO::store(wr + (size_t)(2 * C + j) * ES, q ? FO::mul(ra, r64) : ra);  // r^(j+1), Montgomery
+      FO::store(wm.el(r, 2 * C + j), q ? FO::mul(ra, r64) : ra);  // r^(j+1), Montgomery
       const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
       const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
       bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
-      FO::store(wr + (size_t)(2 * C + c + j) * ES, FO::mul(l0, s0));
-      FO::store(wr + (size_t)(2 * C + 2 * c + j) * ES, FO::sub(FO::mul(l0, s1), half_l));
+      FO::store(wm.el(r, 2 * C + c + j), FO::mul(l0, s0));
+      FO::store(wm.el(r, 2 * C + 2 * c + j), FO::sub(FO::mul(l0, s1), half_l));
     }
   }
   const bool anybad = __any(bad);
   if (lane == 0) {
-    FO::store(wr + (size_t)(2 * C + 3 * c) * ES, gsum);
+    FO::store(wm.el(r, 2 * C + 3 * c), gsum);
     uint8_t* outp = out_prep.at(r);
     if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
     FO::store(outp + (size_t)(1 + arity) * ES, pt);
@@ -1097,6 +1103,211 @@ __global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_
 }
 
 // ------------------------------------------------------------------------------------------------
+// FLP query, ParallelSum types, first half, one LANE per report (Field128).  Same outputs as
+// k_flp_weights_wave, with about half its multiplications and no cross-lane arithmetic:
+//   * Lagrange weights L_k(t) = (alpha^k/m) (t^m - 1) / (t - alpha^k), k = 0..calls, from ONE
+//     batched inversion (Montgomery's trick: prefix products of d_k = t - alpha^k parked in an
+//     element-major scratch, one x^(p-2), a backward pass); t^m - 1 is folded into the inverse,
+//     so each weight costs four multiplications;
+//   * p(t) by Horner, the gadget-output sum sum_d c_d S[d mod m] as a lazily reduced dot product;
+//   * r^(j+1), MM[k] = LM[k] r^(c(k-1)), B0/B1 by running products.
+// Table entries (alpha^k, alpha^k/m, S_i) are wave-uniform (scalar loads).  Memory is moved
+// coalesced in both directions through two per-wave LDS windows of 8 elements x 64 reports (slot
+// 8q + (u ^ ((q >> 1) & 7)) holds element u of report q: each lane's ds_read/write_b128 of its own
+// row is bank-conflict-free, and 8 lanes cover one report's 128 contiguous bytes):
+//   * the proof share (row-major input) arrives by LDS-DMA, 8 reports x 128 B per instruction,
+//     the next window in flight under the arithmetic of the current one;
+//   * the weight rows (row-major, read per report by k_flp_wires) leave 8 entries at a time.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kFwChunk = 8;                  // elements per LDS window
+constexpr uint32_t kFwWin = 64 * kFwChunk * 16;  // bytes per window (one wave)
+constexpr uint32_t kFwThreads = 128;
+
+__global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n, CRows proof,
+                                                            CRows tq, CRows jr, CRows part,
+                                                            Rows out_prep, uint8_t* status, WMat wm,
+                                                            uint8_t* scr) {
+  using FO = Field128Ops;
+  using T = F128;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[(kFwThreads / 64) * 2 * kFwWin];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t r0w = blockIdx.x * blockDim.x + 64u * wv;
+  if (r0w >= n) return;  // wave-uniform
+  uint8_t* win = lds + wv * 2u * kFwWin;  // proof window
+  uint8_t* wout = win + kFwWin;           // output window
+  const uint32_t r = r0w + lane;
+  const bool live = r < n && status[r] == ST_OK;
+  const uint64_t livemask = __ballot(live);
+  const uint32_t rr = r < n ? r : n - 1u;  // clamped: dead lanes compute on a valid row
+  const uint32_t m = cfg.m, logm = cfg.logm, C = cfg.calls, c = cfg.chunk;
+  const uint32_t arity = cfg.arity, total = arity + cfg.gp_len;
+  const uint32_t sw = (lane >> 1) & 7u;   // this lane's swizzle
+  uint8_t* myrow = win + 128u * lane;     // this lane's slots (16 (u ^ sw) within)
+  uint8_t* myout = wout + 128u * lane;
+  auto S = [&](uint32_t k) { return scr + ((size_t)(k - 1u) * n + rr) * 16u; };  // k = 1..C
+  const T one = FO::one_mont();
+  bool bad = false;
+
+  // proof window <- elements [8 ch, 8 ch + 8) of the wave's 64 rows (LDS-DMA instruction i fills
+  // slots [64i, 64i + 64): report 8i + lane/8, element (lane & 7) ^ swizzle)
+  auto stage = [&](uint32_t ch) {
+    uint32_t ln;  // opaque copy (see emit)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    const uint32_t ql = ln >> 3;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+      const uint32_t q = 8u * i + ql;
+      const uint32_t u = (ln & 7u) ^ ((q >> 1) & 7u);
+      const uint32_t row = min(r0w + q, n - 1u);
+      const uint32_t e = min(kFwChunk * ch + u, total - 1u);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(proof.base + (size_t)row * proof.stride +
+                                                          16u * e),
+          (__attribute__((address_space(3))) void*)(win + 1024u * i), 16, 0, 0);
+    }
+  };
+  // weight-row entries [pos, pos + cnt) (cnt <= 8) of every live report of the wave <- v[0..cnt)
+  auto emit = [&](uint32_t pos, const T* v, uint32_t cnt) {
+#pragma unroll
+    for (uint32_t u = 0; u < kFwChunk; ++u)
+      if (u < cnt) FO::store(myout + 16u * (u ^ sw), v[u]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint32_t ln;  // opaque copy: keeps LICM from hoisting 8 row addresses out of the callers' loops
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    const uint32_t ql = ln >> 3, u = ln & 7u;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+      const uint32_t q = 8u * i + ql;
+      const T x = FO::load(wout + 16u * (8u * q + (u ^ ((q >> 1) & 7u))));
+      if (u < cnt && ((livemask >> q) & 1ull)) FO::store(wm.el(r0w + q, pos + u), x);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  const uint32_t nch = (total + kFwChunk - 1u) / kFwChunk;
+  stage(nch - 1u);  // in flight under the Lagrange weights
+
+  const T tm = FO::to_mont(FO::load(tq.at(rr)));
+  T tmm = tm;
+  for (uint32_t i = 0; i < logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
+  const bool tbad = FO::eq(tmm, one);
+
+  // Lagrange weights: prefix products P_k = d_0 ... d_k, P_(k-1) parked in scratch entry k
+  T P = FO::sub(tm, one);  // d_0 (alpha^0 = 1)
+  for (uint32_t k = 1; k <= C; ++k) {
+    FO::store(S(k), P);
+    P = FO::mul(P, FO::sub(tm, ld_tw<FO>(cfg, k)));
+  }
+  T inv = FO::mul(inv_mont128(P), FO::sub(tmm, one));  // (t^m - 1) / (d_0 ... d_C)
+  T lsum = FO::zero();
+  for (uint32_t hi = C + 1u; hi > 1u;) {  // blocks of 8, k = hi - 1 down to lo
+    const uint32_t nb = hi - 1u >= kFwChunk ? kFwChunk : hi - 1u;
+    const uint32_t lo = hi - nb;
+    T pb[kFwChunk];
+#pragma unroll
+    for (uint32_t u = 0; u < kFwChunk; ++u)
+      if (u < nb) pb[u] = FO::load(S(lo + u));
+#pragma unroll
+    for (int u = kFwChunk - 1; u >= 0; --u) {
+      if ((uint32_t)u < nb) {
+        const uint32_t k = lo + (uint32_t)u;
+        pb[u] = FO::mul(FO::mul(inv, pb[u]), ld_tw<FO>(cfg, 2u * m + 1u + k));  // L_k
+        inv = FO::mul(inv, FO::sub(tm, ld_tw<FO>(cfg, k)));
+        FO::store(S(k), pb[u]);
+        lsum = FO::add(lsum, pb[u]);
+      }
+    }
+    emit(C + lo - 1u, pb, nb);  // LM[lo .. lo + nb)
+    hi = lo;
+  }
+  const T l0 = FO::mul(inv, ld_tw<FO>(cfg, 2u * m + 1u));  // k = 0
+  const T half_l = FO::mul(lsum, FO::half());
+
+  // RP[j] = r^(j+1) (Montgomery), then rc = r^c
+  const T rm = FO::to_mont(FO::load(jr.at(rr)));
+  T rp = one;
+  for (uint32_t j0 = 0; j0 < c; j0 += kFwChunk) {
+    T vb[kFwChunk];
+#pragma unroll
+    for (uint32_t u = 0; u < kFwChunk; ++u) {
+      if (j0 + u < c) {
+        rp = FO::mul(rp, rm);
+        vb[u] = rp;
+      }
+    }
+    emit(2 * C + j0, vb, min(kFwChunk, c - j0));
+  }
+  // MM[k] = LM[k] rc^(k-1)
+  T q = one;
+  for (uint32_t k0 = 1; k0 <= C; k0 += kFwChunk) {
+    T vb[kFwChunk];
+#pragma unroll
+    for (uint32_t u = 0; u < kFwChunk; ++u)
+      if (k0 + u <= C) vb[u] = FO::load(S(k0 + u));
+#pragma unroll
+    for (uint32_t u = 0; u < kFwChunk; ++u) {
+      if (k0 + u <= C) {
+        vb[u] = FO::mul(vb[u], q);
+        q = FO::mul(q, rp);
+      }
+    }
+    emit(k0 - 1u, vb, min(kFwChunk, C + 1u - k0));
+  }
+
+  // proof share, last window first: gadget-poly coefficients (Horner needs d descending) and the
+  // wire seeds:  B0[j] = L0 s_2j,  B1[j] = L0 s_2j+1 - (1/2) sum_{k>=1} L_k
+  T pt = FO::zero();
+  Wide gw;
+  wide_zero(gw);
+  for (int ch = (int)nch - 1; ch >= 0; --ch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    T xb[kFwChunk];
+#pragma unroll
+    for (uint32_t u = 0; u < kFwChunk; ++u) xb[u] = FO::load(myrow + 16u * (u ^ sw));
+    if (ch > 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stage((uint32_t)ch - 1u);
+    }
+    const uint32_t e0 = kFwChunk * (uint32_t)ch;  // even: a window holds whole seed pairs
+#pragma unroll
+    for (int u = kFwChunk - 1; u >= 0; --u) {
+      const uint32_t e = e0 + (uint32_t)u;
+      if (e >= total || e < arity) continue;  // wave-uniform
+      bad |= !FO::is_canonical(xb[u]);
+      pt = FO::add(FO::mul(pt, tm), xb[u]);
+      wide_mac(gw, ld_tw<FO>(cfg, m + 1u + ((e - arity) & (m - 1u))), xb[u]);
+    }
+    if (e0 < arity) {  // wave-uniform
+      const uint32_t np = min(kFwChunk, arity - e0) / 2u;  // seed pairs in this window
+      T bv[kFwChunk / 2];
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+        for (uint32_t u = 0; u < kFwChunk / 2; ++u) {
+          if (u < np) {
+            const T x = xb[2 * u + h];
+            bad |= !FO::is_canonical(x);
+            bv[u] = h ? FO::sub(FO::mul(l0, x), half_l) : FO::mul(l0, x);
+          }
+        }
+        emit(2 * C + (1u + h) * c + e0 / 2u, bv, np);
+      }
+    }
+  }
+  const T gsum = wide_reduce(gw);
+  if (!live) return;
+  FO::store(wm.el(rr, 2 * C + 3 * c), gsum);
+  uint8_t* outp = out_prep.at(rr);
+  if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
+  FO::store(outp + (size_t)(1 + arity) * 16, pt);
+  const uint8_t* pp = part.at(rr);
+  uint8_t* dst = outp + (size_t)cfg.verifier_len * 16;
+  st64(dst, ld64(pp));
+  st64(dst + 8, ld64(pp + 8));
+  if (bad) status[rr] = ST_INVALID_MESSAGE;
+  else if (tbad) status[rr] = ST_VDAF_PREP_ERROR;
+}
+
+// ------------------------------------------------------------------------------------------------
 // FLP query, ParallelSum types, second half: stream the measurement share once and form the wires
 //   wire_2j   = B0[j] + r^(j+1) sum_k MM[k] x_(k-1)c+j      wire_2j+1 = B1[j] + sum_k LM[k] x_(k-1)c+j
 // (weights from k_flp_query's split mode).  Block per report, thread (h, j): column j, calls
@@ -1104,7 +1315,7 @@ __global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights(Cfg cfg, uint32_
 // ------------------------------------------------------------------------------------------------
 template <class FO>
 __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
-                                                   CRows wrows, CRows jr, Rows out_prep,
+                                                   WMat wm, CRows jr, Rows out_prep,
                                                    uint8_t* status) {
   using T = typename FO::T;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1121,8 +1332,7 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
   T* RED = PB + H * c;
   uint32_t* flag = reinterpret_cast<uint32_t*>(RED + nthr);
   if (tid == 0) *flag = 0u;
-  const uint8_t* wr = wrows.at(r);
-  for (uint32_t k = tid; k < 2 * C; k += nthr) MM[k] = FO::load(wr + (size_t)k * ES);
+  for (uint32_t k = tid; k < 2 * C; k += nthr) MM[k] = FO::load(wm.el(r, k));
   __syncthreads();
   const uint8_t* xr = meas.at(r);
   bool bad = false;
@@ -1183,9 +1393,9 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
       a = FO::add(a, PA[h * c + j]);
       b = FO::add(b, PB[h * c + j]);
     }
-    const T rp = FO::load(wr + (size_t)(2 * C + j) * ES);  // Montgomery
-    const T w0 = FO::add(FO::load(wr + (size_t)(2 * C + c + j) * ES), FO::mul(rp, a));
-    const T w1 = FO::add(FO::load(wr + (size_t)(2 * C + 2 * c + j) * ES), b);
+    const T rp = FO::load(wm.el(r, 2 * C + j));  // Montgomery
+    const T w0 = FO::add(FO::load(wm.el(r, 2 * C + c + j)), FO::mul(rp, a));
+    const T w1 = FO::add(FO::load(wm.el(r, 2 * C + 2 * c + j)), b);
     FO::store(outp + (size_t)(1 + 2 * j) * ES, w0);
     FO::store(outp + (size_t)(2 + 2 * j) * ES, w1);
   }
@@ -1195,7 +1405,7 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
   if (tid == 0) {
     if (cfg.kind == KIND_HISTOGRAM) {
       // v = jr[1] * range + jr[1]^2 * (sum x - 1/2)
-      const T gsum = FO::load(wr + (size_t)(2 * C + 3 * c) * ES);
+      const T gsum = FO::load(wm.el(r, 2 * C + 3 * c));
       const T r1m = FO::to_mont(FO::load(jr.at(r) + ES));
       const T sc = FO::sub(xsum, FO::half());
       FO::store(outp, FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc)));
