@@ -203,6 +203,41 @@ def encode_agg_init_req(query_type: int, batch_id: Optional[bytes], agg_param: b
     return out.tobytes()
 
 
+def encode_agg_init_req_packed(query_type: int, batch_id: Optional[bytes], agg_param: bytes,
+                               nonces: np.ndarray, times, public_shares: Optional[np.ndarray],
+                               hpke_config_ids: np.ndarray, encs: np.ndarray,
+                               enc_offsets: np.ndarray, payloads: np.ndarray,
+                               payload_offsets: np.ndarray, prep_shares: np.ndarray,
+                               status: Optional[np.ndarray] = None) -> bytes:
+    """As encode_agg_init_req, with the helper ciphertexts already packed (config ids, one buffer
+    of encapsulated keys + (n + 1) offsets, one buffer of payloads + offsets): no per-report
+    Python work, for whole aggregation jobs."""
+    n = len(nonces)
+    nonces = np.ascontiguousarray(nonces, np.uint8)
+    tm = np.ascontiguousarray(times, np.uint64)
+    pub = None if public_shares is None else np.ascontiguousarray(public_shares, np.uint8)
+    pub_len = pub.shape[1] if pub is not None and pub.ndim == 2 else 0
+    cids = np.ascontiguousarray(hpke_config_ids, np.uint8)
+    eb = np.ascontiguousarray(encs, np.uint8)
+    eo = np.ascontiguousarray(enc_offsets, np.uint64)
+    pb = np.ascontiguousarray(payloads, np.uint8)
+    po = np.ascontiguousarray(payload_offsets, np.uint64)
+    ps = np.ascontiguousarray(prep_shares, np.uint8)
+    if len(tm) != n or len(cids) != n or len(eo) != n + 1 or len(po) != n + 1 or len(ps) != n:
+        raise ValueError("per-report arrays disagree on the report count")
+    st = None if status is None else np.ascontiguousarray(status, np.uint8)
+    ap = np.frombuffer(bytes(agg_param) or b"\0", np.uint8).copy()
+    bid = None if batch_id is None else np.frombuffer(bytes(batch_id), np.uint8).copy()
+    args = lambda out, cap, ln: (query_type, _p(bid), _p(ap), len(agg_param), n, _p(nonces),
+                                 _p(tm), _p(pub), pub_len, _p(cids), _p(eb), _p(eo), _p(pb),
+                                 _p(po), _p(ps), ps.shape[1], _p(st), out, cap, ctypes.byref(ln))
+    ln = ctypes.c_size_t()
+    check(lib().prio3gpu_encode_agg_init_req(*args(None, 0, ln)), "encode init req")
+    out = np.empty(ln.value, np.uint8)
+    check(lib().prio3gpu_encode_agg_init_req(*args(_p(out), out.size, ln)), "encode init req")
+    return out.tobytes()
+
+
 def decode_agg_job_resp(msg: bytes):
     raw = _u8(msg).copy()
     n = ctypes.c_size_t()

@@ -363,33 +363,60 @@ int prio3gpu_encode_agg_init_req(int query_type, const uint8_t* batch_id, const 
   w.bytes(agg_param, agg_param_len);
   w.be((uint64_t)query_type, 1);
   if (query_type == 2) w.bytes(batch_id, 32);
+  auto item_len = [&](size_t i) -> size_t {
+    return 16 + 8 + 4 + public_share_len + 1 + 2 + (size_t)(enc_offsets[i + 1] - enc_offsets[i]) +
+           4 + (size_t)(payload_offsets[i + 1] - payload_offsets[i]) + 1 + 4 + prep_share_len;
+  };
   size_t items = 0;
-  for (size_t i = 0; i < n; ++i) {
-    if (status && status[i]) continue;  // reports that failed leader prepare_init are not sent
-    items += 16 + 8 + 4 + public_share_len + 1 + 2 + (enc_offsets[i + 1] - enc_offsets[i]) + 4 +
-             (payload_offsets[i + 1] - payload_offsets[i]) + 1 + 4 + prep_share_len;
-  }
+  for (size_t i = 0; i < n; ++i)
+    if (!(status && status[i])) items += item_len(i);  // failed leader prepare_init: not sent
   w.be(items, 4);
-  for (size_t i = 0; i < n; ++i) {
-    if (status && status[i]) continue;
-    w.bytes(nonces + 16 * i, 16);
-    w.be(times[i], 8);
-    w.be(public_share_len, 4);
-    w.bytes(public_shares ? public_shares + (size_t)public_share_len * i : nullptr,
-            public_share_len);
-    w.be(hpke_config_ids[i], 1);
-    const size_t el = (size_t)(enc_offsets[i + 1] - enc_offsets[i]);
-    w.be(el, 2);
-    w.bytes(encs + enc_offsets[i], el);
-    const size_t pl = (size_t)(payload_offsets[i + 1] - payload_offsets[i]);
-    w.be(pl, 4);
-    w.bytes(payloads + payload_offsets[i], pl);
-    w.be(0, 1);  // PingPongMessage::Initialize { prep_share }
-    w.be(prep_share_len, 4);
-    w.bytes(prep_shares + (size_t)prep_share_len * i, prep_share_len);
+  const size_t body = w.off;
+  *out_len = body + items;
+  if (!out) return 0;
+  if (*out_len > cap) return PRIO3GPU_E_CAPACITY;
+  // PrepareInit i is written at its own offset: large jobs (SumVec: ~3 KB per report) are
+  // encoded on up to 8 threads over report ranges, each range starting at its prefix offset.
+  auto run = [&](size_t lo, size_t hi, size_t at) {
+    Writer x(out + at, cap - at);
+    for (size_t i = lo; i < hi; ++i) {
+      if (status && status[i]) continue;
+      x.bytes(nonces + 16 * i, 16);
+      x.be(times[i], 8);
+      x.be(public_share_len, 4);
+      x.bytes(public_shares ? public_shares + (size_t)public_share_len * i : nullptr,
+              public_share_len);
+      x.be(hpke_config_ids[i], 1);
+      const size_t el = (size_t)(enc_offsets[i + 1] - enc_offsets[i]);
+      x.be(el, 2);
+      x.bytes(encs + enc_offsets[i], el);
+      const size_t pl = (size_t)(payload_offsets[i + 1] - payload_offsets[i]);
+      x.be(pl, 4);
+      x.bytes(payloads + payload_offsets[i], pl);
+      x.be(0, 1);  // PingPongMessage::Initialize { prep_share }
+      x.be(prep_share_len, 4);
+      x.bytes(prep_shares + (size_t)prep_share_len * i, prep_share_len);
+    }
+  };
+  const size_t nt = items < (size_t(8) << 20) ? 1 : std::min<size_t>(8, (n + 4095) / 4096);
+  if (nt <= 1) {
+    run(0, n, body);
+    return 0;
   }
-  *out_len = w.off;
-  return (out && w.off > cap) ? PRIO3GPU_E_CAPACITY : 0;
+  const size_t per = (n + nt - 1) / nt;
+  std::vector<size_t> start(nt, body);
+  for (size_t t = 1; t < nt; ++t) {
+    size_t acc = start[t - 1];
+    for (size_t i = (t - 1) * per; i < std::min(n, t * per); ++i)
+      if (!(status && status[i])) acc += item_len(i);
+    start[t] = acc;
+  }
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < nt; ++t)
+    pool.emplace_back(run, std::min(n, t * per), std::min(n, (t + 1) * per), start[t]);
+  run(0, std::min(n, per), body);
+  for (auto& th : pool) th.join();
+  return 0;
 }
 
 int prio3gpu_decode_agg_job_resp(const uint8_t* msg, size_t len,

@@ -1,0 +1,258 @@
+"""Batched leader aggregate-init driver: the host-side mirror of Janus's
+`AggregationJobDriver::step_aggregation_job_aggregate_init` + `process_response_from_helper`
+(aggregator/src/aggregator/aggregation_job_driver.rs:290-437, :530-727) for one task, minus the
+datastore transactions and the HTTP client (out of scope): the helper round trip is
+a caller-supplied `send(request_bytes) -> response_bytes`.
+
+Per aggregation job (the job's `LeaderStoredReport`s, models.rs:78, already decoded from the
+datastore as in aggregator_core/src/datastore.rs:1298-1304):
+  1. per-report pre-checks: a missing client report -> ReportDropped (2) (:330-342), repeated
+     leader extensions -> InvalidMessage (8) (:344-359)
+  2. prio3gpu_prepare_init(agg_id 0) on the GPU (`leader_initialized`, :362-380); reports it
+     rejects -> VdafPrepError (5) / InvalidMessage (8), never sent
+  3. AggregationJobInitializeReq of the surviving reports: ReportShare (metadata, public share,
+     the helper's encrypted input share) + PingPongMessage::Initialize{prep share} (:382-411)
+  4. send to the helper
+  5. AggregationJobResp: the response must answer exactly the sent reports, in order, else the
+     whole job fails (:556-573); Continue{Finish{prep msg}} -> prio3gpu_prepare_next
+     (`leader_continued` -> FinishedNoMessage) + accumulate (:575-627); Finished while the
+     leader is not finished -> VdafPrepError (:632-664); Reject(e) -> e (:666-677)
+  6. Accumulator::update bookkeeping: report-ID checksum + client-timestamp interval per batch
+     slot (accumulator.rs:76-122)
+
+`run_jobs` pipelines a stream of jobs the way Janus runs aggregation jobs concurrently
+(job_driver.rs:119-216): the host -> GPU copy of job k+1's leader input shares (the dominant
+input, 134,944 B per SumVec(8,1000) report; pinned host memory, its own copy stream) overlaps
+the GPU preparation of job k, and the helper round trip of job k overlaps the GPU work of job
+k+1.  Returns per-report final statuses (0 = Finished).
+"""
+from __future__ import annotations
+
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from . import codec as C
+from ._lib import EmptyAggregation
+from .prio3 import AggregateShares, PrepareState, Prio3Gpu
+
+REPORT_DROPPED, VDAF_PREP_ERROR, INVALID_MESSAGE = 2, 5, 8
+
+
+@dataclass
+class LeaderJob:
+    """One aggregation job's reports, columnar (report i = row i)."""
+    nonces: np.ndarray               # (n, 16) report IDs (the VDAF nonces)
+    times: np.ndarray                # (n,) u64 client timestamps
+    public: np.ndarray               # (n, public_share) encoded public shares
+    leader_in: object                # (n, leader_input_share) uint8: numpy (pinned: see
+                                     # LeaderAggregateInit.pinned) or a torch tensor on the GPU
+    hpke_config_ids: np.ndarray      # (n,) helper ciphertext config ids
+    encs: np.ndarray                 # concatenated encapsulated keys
+    enc_offsets: np.ndarray          # (n + 1,) u64
+    payloads: np.ndarray             # concatenated helper ciphertext payloads
+    payload_offsets: np.ndarray      # (n + 1,) u64
+    present: Optional[np.ndarray] = None         # (n,) bool; False: report garbage-collected
+    dup_extensions: Optional[np.ndarray] = None  # (n,) bool; True: repeated leader extension
+
+    @property
+    def n(self) -> int:
+        return len(self.nonces)
+
+    @staticmethod
+    def pack_ciphertexts(cts: Sequence[tuple]):
+        """[(config id, enc, payload)] -> (ids, encs, enc_offsets, payloads, payload_offsets)."""
+        n = len(cts)
+        ids = np.array([c[0] for c in cts], np.uint8)
+        eo = np.zeros(n + 1, np.uint64)
+        eo[1:] = np.cumsum([len(c[1]) for c in cts])
+        po = np.zeros(n + 1, np.uint64)
+        po[1:] = np.cumsum([len(c[2]) for c in cts])
+        eb = np.frombuffer(b"".join(bytes(c[1]) for c in cts) or b"\0", np.uint8).copy()
+        pb = np.frombuffer(b"".join(bytes(c[2]) for c in cts) or b"\0", np.uint8).copy()
+        return ids, eb, eo, pb, po
+
+
+@dataclass
+class LeaderStepped:
+    """A job between its request and the helper's response (Janus: SteppedAggregation list)."""
+    job: LeaderJob
+    state: PrepareState
+    status: np.ndarray
+    request: bytes
+    d_in: object = None              # device copy of the leader input shares (kept alive)
+    slots: Optional[np.ndarray] = None
+    times_ms: dict = field(default_factory=dict)
+
+
+class LeaderAggregateInit:
+    def __init__(self, vdaf: Prio3Gpu, query_type: int = C.TIME_INTERVAL,
+                 batch_id: Optional[bytes] = None,
+                 batch_slot_of: Optional[Callable[[np.ndarray], np.ndarray]] = None):
+        """`batch_slot_of(times) -> slots` maps report times to aggregate slots (Janus's
+        partial batch identifier per report); None = one slot."""
+        if query_type == C.FIXED_SIZE and batch_id is None:
+            raise ValueError("fixed-size aggregation jobs carry a batch id")
+        self.vdaf = vdaf
+        self.query_type = query_type
+        self.batch_id = batch_id
+        self.batch_slot_of = batch_slot_of
+        self._copy_stream = None
+        self._lock = threading.Lock()
+        self._prep_bufs: List[np.ndarray] = []  # pinned prep-share buffers, one per job in flight
+        # prepare states of the jobs in flight, reused: creating / destroying one allocates /
+        # frees device memory, and hipFree waits for the whole device (the next job's H2D copy)
+        self._states: List[PrepareState] = []
+
+    # -- host staging --------------------------------------------------------------------------------
+    @staticmethod
+    def pinned(n: int, width: int) -> np.ndarray:
+        """A pinned (page-locked) (n, width) uint8 host array, for decoding leader input shares
+        into so that the host -> GPU copy is DMA."""
+        import torch
+        # the ndarray's base keeps the tensor (and its pinned allocation) alive
+        return torch.empty((n, width), dtype=torch.uint8, pin_memory=True).numpy()
+
+    def stage(self, job: LeaderJob):
+        """Copy the job's leader input shares to the GPU on the driver's copy stream (blocking
+        this thread only); a torch CUDA tensor is used as is."""
+        import torch
+        li = job.leader_in
+        if isinstance(li, torch.Tensor) and li.is_cuda:
+            return li
+        with self._lock:
+            if self._copy_stream is None:
+                self._copy_stream = torch.cuda.Stream(device=self.vdaf.device)
+        s = self._copy_stream
+        src = torch.from_numpy(np.ascontiguousarray(li))
+        with torch.cuda.stream(s):
+            d = torch.empty(src.shape, dtype=torch.uint8, device=f"cuda:{self.vdaf.device}")
+            d.copy_(src, non_blocking=True)
+        s.synchronize()
+        return d
+
+    def _state(self, n: int) -> PrepareState:
+        with self._lock:
+            for k, st in enumerate(self._states):
+                if st.capacity >= n:
+                    return self._states.pop(k)
+        return self.vdaf.new_state(0, n)
+
+    def _release(self, st: PrepareState):
+        with self._lock:
+            self._states.append(st)
+
+    def close(self):
+        with self._lock:
+            for st in self._states:
+                st.close()
+            self._states = []
+            self._prep_bufs = []
+
+    def _prep_buf(self, n: int) -> np.ndarray:
+        """A pinned (>= n, prep_share) buffer for prepare_init's output (the device -> host copy
+        of 2,896 B per SumVec report is then DMA); buffers are reused once the request that
+        copied them out has been encoded."""
+        w = self.vdaf.sizes.prep_share
+        with self._lock:
+            for k, b in enumerate(self._prep_bufs):
+                if b.shape[0] >= n:
+                    return self._prep_bufs.pop(k)
+        try:
+            return self.pinned(max(n, 1024), w)
+        except RuntimeError:  # no GPU runtime for pinning: pageable memory
+            return np.zeros((max(n, 1024), w), np.uint8)
+
+    # -- steps ---------------------------------------------------------------------------------------
+    def init(self, job: LeaderJob, d_in=None) -> LeaderStepped:
+        """Steps 1-3: pre-checks, GPU prepare_init, request bytes."""
+        import time
+        n = job.n
+        if n == 0:
+            raise EmptyAggregation("aggregation job contains no reports")
+        s = self.vdaf.sizes
+        t0 = time.perf_counter()
+        status = np.zeros(n, np.uint8)
+        if job.present is not None:
+            status[~np.asarray(job.present, bool)] = REPORT_DROPPED
+        if job.dup_extensions is not None:
+            status[(status == 0) & np.asarray(job.dup_extensions, bool)] = INVALID_MESSAGE
+        if d_in is None:
+            d_in = self.stage(job)
+        t1 = time.perf_counter()
+        state = self._state(n)
+        pbuf = self._prep_buf(n)
+        try:
+            prep, status = self.vdaf.prepare_init(state, job.nonces,
+                                                  job.public if s.public_share else None, d_in,
+                                                  status=status, out_prep_shares=pbuf)
+            t2 = time.perf_counter()
+            req = C.encode_agg_init_req_packed(self.query_type, self.batch_id, b"", job.nonces,
+                                               job.times, job.public, job.hpke_config_ids,
+                                               job.encs, job.enc_offsets, job.payloads,
+                                               job.payload_offsets, prep, status)
+        except BaseException:
+            self._release(state)
+            raise
+        finally:
+            self._prep_bufs.append(pbuf)  # the prep shares live on in the request bytes
+        t3 = time.perf_counter()
+        slots = None
+        if self.batch_slot_of is not None:
+            slots = np.ascontiguousarray(self.batch_slot_of(np.asarray(job.times)), np.uint32)
+        return LeaderStepped(job, state, status, req, d_in, slots,
+                             {"stage": (t1 - t0) * 1e3, "prepare_init": (t2 - t1) * 1e3,
+                              "encode": (t3 - t2) * 1e3})
+
+    def finish(self, st: LeaderStepped, resp: bytes, agg: AggregateShares) -> np.ndarray:
+        """Steps 5-6.  Raises Prio3GpuError when the response does not answer exactly the sent
+        reports in order (the whole job fails, aggregation_job_driver.rs:556-573)."""
+        import time
+        t0 = time.perf_counter()
+        try:
+            pm, status = C.gather_helper_resps(self.vdaf.sizes, resp, st.job.nonces,
+                                               st.status.copy())
+            t1 = time.perf_counter()
+            self.vdaf.prepare_next(st.state, pm, status, want_output_shares=False, agg=agg,
+                                   batch_slots=st.slots)
+            agg.update_reports(st.job.nonces, st.job.times, status, st.slots)
+            t2 = time.perf_counter()
+        finally:
+            self._release(st.state)
+            st.d_in = None
+        st.times_ms.update({"decode": (t1 - t0) * 1e3, "prepare_next": (t2 - t1) * 1e3})
+        return status
+
+    def handle(self, job: LeaderJob, send: Callable[[bytes], bytes],
+               agg: AggregateShares) -> np.ndarray:
+        st = self.init(job)
+        return self.finish(st, send(st.request), agg)
+
+    def run_jobs(self, jobs: Sequence[LeaderJob], send: Callable[[bytes], bytes],
+                 agg: AggregateShares, stats: Optional[list] = None) -> List[np.ndarray]:
+        """Pipelined over jobs: H2D of job k+1 || GPU prepare_init of job k; helper round trip
+        of job k || GPU work of job k+1.  `stats`, if given, receives each job's stage times."""
+        out: List[np.ndarray] = []
+        if not jobs:
+            return out
+        with ThreadPoolExecutor(max_workers=1) as h2d, ThreadPoolExecutor(max_workers=1) as net:
+            staged = h2d.submit(self.stage, jobs[0])
+            inflight = None
+            for k in range(len(jobs)):
+                d_in = staged.result()
+                if k + 1 < len(jobs):
+                    staged = h2d.submit(self.stage, jobs[k + 1])
+                st = self.init(jobs[k], d_in)
+                fut = net.submit(send, st.request)
+                if inflight is not None:
+                    out.append(self.finish(inflight[0], inflight[1].result(), agg))
+                    if stats is not None:
+                        stats.append(inflight[0].times_ms)
+                inflight = (st, fut)
+            out.append(self.finish(inflight[0], inflight[1].result(), agg))
+            if stats is not None:
+                stats.append(inflight[0].times_ms)
+        return out

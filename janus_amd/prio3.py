@@ -276,8 +276,10 @@ class Prio3Gpu:
 
     # -- Aggregator --------------------------------------------------------------------------------
     def prepare_init(self, state: PrepareState, nonces, public_shares, input_shares,
-                     status=None, want_prep_shares: bool = True):
-        """Batched `prepare_init` -> (prep_shares (n, prep_share) uint8, status (n,) uint8)."""
+                     status=None, want_prep_shares: bool = True, out_prep_shares=None):
+        """Batched `prepare_init` -> (prep_shares (n, prep_share) uint8, status (n,) uint8).
+        `out_prep_shares`: optional (>= n, prep_share) uint8 destination (e.g. pinned host
+        memory, so the device -> host copy is DMA)."""
         s = self.sizes
         n = _nbytes(nonces) // 16
         in_len = s.leader_input_share if state.agg_id == 0 else s.helper_input_share
@@ -286,7 +288,13 @@ class Prio3Gpu:
             if s.public_share else None
         input_shares = _as_u8(input_shares, n, in_len, "input shares")
         st = np.zeros(n, dtype=np.uint8) if status is None else status
-        prep = np.zeros((n, s.prep_share), dtype=np.uint8) if want_prep_shares else None
+        if out_prep_shares is not None:
+            prep = out_prep_shares[:n]
+            if prep.shape != (n, s.prep_share) or prep.dtype != np.uint8 or \
+                    not prep.flags.c_contiguous:
+                raise ValueError("out_prep_shares must be a contiguous (n, prep_share) uint8 array")
+        else:
+            prep = np.zeros((n, s.prep_share), dtype=np.uint8) if want_prep_shares else None
         check(lib().prio3gpu_prepare_init(self._ctx, state._h, n, _ptr(nonces),
                                           _ptr(public_shares), _ptr(input_shares), _ptr(prep),
                                           _ptr(st)), "prepare_init")

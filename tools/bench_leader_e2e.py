@@ -1,0 +1,136 @@
+"""End-to-end leader aggregate-init throughput on one GPU (SURVEY §8(a) A2 with its host stages):
+decoded leader input shares in pinned host memory -> H2D on a copy stream -> GPU prepare_init
+(agg_id 0) -> AggregationJobInitializeReq bytes -> [helper round trip] -> AggregationJobResp bytes
+-> gather prep msgs -> GPU prepare_next + accumulate + report bookkeeping, pipelined over jobs by
+LeaderAggregateInit.run_jobs.  Prio3SumVec(8, 1000, 89).
+
+Inputs (all made before timing): seeded random nonces, client randomness and measurements, shares
+from the GPU client shard; the helper's encrypted input shares are random bytes of the real sizes
+(32-B X25519 encapsulated key, 70-B AES-GCM payload: the leader forwards them unopened); the
+helper's responses are computed beforehand by the GPU helper path (prio3gpu_helper_init), so
+`send` returns them with no network or helper time -- the number is the leader's own bound.
+
+  python tools/bench_leader_e2e.py --jobs 4 --job-size 32768
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from bench import CONFIGS  # noqa: E402
+from janus_amd import codec as C  # noqa: E402
+from janus_amd.leader import LeaderAggregateInit, LeaderJob  # noqa: E402
+from janus_amd.prio3 import Prio3Gpu  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=4)
+    ap.add_argument("--job-size", type=int, default=32768)
+    ap.add_argument("--reps", type=int, default=2)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    kind, bits, length, chunk, label = CONFIGS["sumvec"]
+    cfg_id = b"bench-sumvec"
+    vk = hashlib.shake_128(b"verify-key" + cfg_id).digest(16)
+    v = Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=0)
+    hv = Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=0)
+    s = v.sizes
+    M, J = args.job_size, args.jobs
+    rng = np.random.default_rng(2025)
+    drv = LeaderAggregateInit(v)
+    t0 = time.time()
+    jobs, resps, plain = [], {}, np.zeros(length, np.int64)
+    ls, hs, ss = v.new_state(0, M), hv.new_state(1, M), v.new_state(1, M)
+    hagg = hv.new_aggregate(1)  # each job's helper aggregate, once (for the parity check)
+    for j in range(J):
+        nonces = rng.integers(0, 256, (M, 16), dtype=np.uint8)
+        meas = rng.integers(0, 1 << bits, (M, length), dtype=np.int64)
+        plain += meas.sum(axis=0)
+        d_nonces = torch.from_numpy(nonces).to(dev)
+        d_rand = torch.from_numpy(rng.integers(0, 256, (M, v.random_size()), dtype=np.uint8)).to(dev)
+        d_pub = torch.empty((M, s.public_share), dtype=torch.uint8, device=dev)
+        d_lin = torch.empty((M, s.leader_input_share), dtype=torch.uint8, device=dev)
+        d_hin = torch.empty((M, s.helper_input_share), dtype=torch.uint8, device=dev)
+        v.shard(ss, d_nonces, torch.from_numpy(meas).to(dev), d_rand, out=(d_pub, d_lin, d_hin))
+        # the helper's answer for this job (GPU helper path), precomputed
+        lp, lst = v.prepare_init(ls, d_nonces, d_pub, d_lin)
+        msgs, hst = hv.helper_init(hs, d_nonces, d_pub, d_hin, lp, agg=hagg)
+        assert (lst == 0).all() and (hst == 0).all()
+        pin = drv.pinned(M, s.leader_input_share)
+        pin[:] = d_lin.cpu().numpy()  # "decoded from the datastore" into pinned memory
+        times = (1_700_000_000 + (np.arange(M) + j * M) % 3600).astype(np.uint64)
+        ids = np.ones(M, np.uint8)
+        eo = (np.arange(M + 1) * 32).astype(np.uint64)
+        po = (np.arange(M + 1) * 70).astype(np.uint64)
+        job = LeaderJob(nonces, times, d_pub.cpu().numpy(), pin, ids,
+                        rng.integers(0, 256, 32 * M, dtype=np.uint8), eo,
+                        rng.integers(0, 256, 70 * M, dtype=np.uint8), po)
+        jobs.append(job)
+        resps[nonces[:1].tobytes()] = C.encode_agg_job_resp(nonces, msgs, s.prep_msg, hst)
+        del d_lin, d_rand, d_hin
+    for x in (ls, hs, ss):
+        x.close()
+    gen_s = time.time() - t0
+
+    def send(req: bytes) -> bytes:  # the helper, answered from the precomputed responses
+        d = C.decode_agg_init_req(req)
+        return resps[d.raw[d.views[0].report_id_off:d.views[0].report_id_off + 16].tobytes()]
+
+    agg = v.new_aggregate(1)
+    drv.run_jobs(jobs[:1], send, agg)  # warm
+    agg = v.new_aggregate(1)
+    stats = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        sts = drv.run_jobs(jobs, send, agg, stats=stats)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n = J * M * args.reps
+    assert all((st == 0).all() for st in sts)
+    share, cnt = agg.read(0)
+    assert cnt == n, (cnt, n)
+    # parity: leader aggregate (every job reps times) + reps x helper aggregate == reps x plaintext
+    hshare, hcnt = hagg.read(0)
+    P = v.modulus
+    tot = [(a + args.reps * b) % P for a, b in zip(v.decode_field_vec(share),
+                                                    v.decode_field_vec(hshare))]
+    totb = b"".join(int(x).to_bytes(16, "little") for x in tot)
+    zero = bytes(len(totb))
+    assert v.unshard([totb, zero]) == [int(x) * args.reps for x in plain], "aggregate != plaintext"
+    stage = {k: round(float(np.mean([x[k] for x in stats])), 2) for k in stats[0]}
+    req_mb = round(len(C.encode_agg_init_req_packed(
+        C.TIME_INTERVAL, None, b"", jobs[0].nonces, jobs[0].times, jobs[0].public,
+        jobs[0].hpke_config_ids, jobs[0].encs, jobs[0].enc_offsets, jobs[0].payloads,
+        jobs[0].payload_offsets, np.zeros((M, s.prep_share), np.uint8))) / 1e6, 1)
+    # unpipelined H2D of one job from pinned memory on the copy stream
+    t = time.perf_counter()
+    d = drv.stage(jobs[0])
+    torch.cuda.synchronize()
+    h2d_s = time.perf_counter() - t
+    del d
+    print(json.dumps({
+        "what": "leader aggregate-init end to end: pinned leader input shares -> H2D -> GPU "
+                "prepare_init -> request bytes -> [precomputed helper response] -> gather -> GPU "
+                "prepare_next + accumulate + report bookkeeping, pipelined over jobs",
+        "value": round(n / dt, 1), "unit": "reports/s", "jobs": J, "job_size": M,
+        "reps": args.reps, "seconds": round(dt, 3),
+        "request_mb_per_job": req_mb,
+        "h2d_gb_per_job": round(M * s.leader_input_share / 1e9, 2),
+        "h2d_gbs_unpipelined": round(M * s.leader_input_share / h2d_s / 1e9, 1),
+        "pcie_bound_reports_per_s": round(M / h2d_s, 1),
+        "stage_ms_per_job_in_pipeline": stage, "gen_seconds": round(gen_s, 1),
+        "workload": label, "parity": "leader + helper aggregate unshards to the plaintext sum"}))
+
+
+if __name__ == "__main__":
+    main()
