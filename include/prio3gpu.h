@@ -114,6 +114,15 @@ typedef struct prio3gpu_sizes {
  * `device` = HIP device ordinal. */
 int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,
                         const uint8_t verify_key[16], int device, prio3gpu_ctx** out);
+/* The XOF behind every Prio3 stream of a context.  PRIO3GPU_XOF_SHAKE128 is prio 0.15.1's
+ * XofShake128 (VDAF-07; what Janus 0.6 runs, aggregator/src/aggregator.rs:73) and the default of
+ * prio3gpu_ctx_create.  PRIO3GPU_XOF_TURBOSHAKE128 is draft-irtf-cfrg-vdaf-08+'s
+ * XofTurboShake128 (Keccak-p[1600, 12], domain byte 0x01) over the same message framing, with the
+ * rest of Prio3 unchanged: a forward-compatibility mode, parity unpinned (no reference vectors). */
+#define PRIO3GPU_XOF_SHAKE128 0
+#define PRIO3GPU_XOF_TURBOSHAKE128 1
+int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,
+                         const uint8_t verify_key[16], int device, int xof, prio3gpu_ctx** out);
 int prio3gpu_ctx_destroy(prio3gpu_ctx* ctx);
 int prio3gpu_ctx_sizes(const prio3gpu_ctx* ctx, prio3gpu_sizes* out);
 /* Wait for all work queued on the context's stream. */

@@ -64,6 +64,8 @@ def _declare(lib):
     sigs = {
         "prio3gpu_ctx_create": (c.c_int, [c.c_int, c.c_uint32, c.c_uint32, c.c_uint32, c.c_char_p,
                                           c.c_int, c.POINTER(P)]),
+        "prio3gpu_ctx_create2": (c.c_int, [c.c_int, c.c_uint32, c.c_uint32, c.c_uint32,
+                                           c.c_char_p, c.c_int, c.c_int, c.POINTER(P)]),
         "prio3gpu_ctx_destroy": (c.c_int, [P]),
         "prio3gpu_ctx_sizes": (c.c_int, [P, P]),
         "prio3gpu_ctx_sync": (c.c_int, [P]),
@@ -141,7 +143,8 @@ def _declare(lib):
 
 # Every symbol include/prio3gpu.h declares (checked by tests/test_abi.py).
 EXPORTED = [
-    "prio3gpu_ctx_create", "prio3gpu_ctx_destroy", "prio3gpu_ctx_sizes", "prio3gpu_ctx_sync",
+    "prio3gpu_ctx_create", "prio3gpu_ctx_create2", "prio3gpu_ctx_destroy", "prio3gpu_ctx_sizes",
+    "prio3gpu_ctx_sync",
     "prio3gpu_ctx_stream", "prio3gpu_state_create", "prio3gpu_state_destroy",
     "prio3gpu_agg_create", "prio3gpu_agg_destroy", "prio3gpu_agg_reset", "prio3gpu_agg_read",
     "prio3gpu_agg_merge_bytes", "prio3gpu_agg_update_reports", "prio3gpu_agg_read_reports",

@@ -950,8 +950,18 @@ const char* prio3gpu_last_error(void) { return g_err.c_str(); }
 
 int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,
                         const uint8_t verify_key[16], int device, prio3gpu_ctx** out) {
+  return prio3gpu_ctx_create2(kind, bits, length, chunk_length, verify_key, device,
+                              PRIO3GPU_XOF_SHAKE128, out);
+}
+
+int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,
+                         const uint8_t verify_key[16], int device, int xof, prio3gpu_ctx** out) {
   if (!out || !verify_key) {
     set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  if (xof != PRIO3GPU_XOF_SHAKE128 && xof != PRIO3GPU_XOF_TURBOSHAKE128) {
+    set_err("unknown XOF %d", xof);
     return PRIO3GPU_E_ARG;
   }
   *out = nullptr;
@@ -984,6 +994,7 @@ int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk
     return rc;
   }
   c->cfg.exact_squeeze = exact_squeeze ? 1u : 0u;
+  c->cfg.xof = xof == PRIO3GPU_XOF_TURBOSHAKE128 ? kXofTurboShake128 : kXofShake128;
   *out = c;
   return 0;
 }

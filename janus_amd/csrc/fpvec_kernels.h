@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
   const int64_t total = 42 + 8 * nd;                // consumer's message bytes before padding
   const int64_t nblocks = total / 168 + 1;          // consumer blocks
   const int64_t padw = total >> 3;
-  const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
+  const uint64_t padv = (uint64_t)cfg.xof.pad << ((total & 7) * 8);
   const uint64_t nonce_hi = ld64(nonces.at(rr) + 8);
   uint64_t s[25];
   if (producer) {
@@ -76,8 +76,8 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
     m.clear();
     m.header(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8));
     m.put8(25, 1u);
-    m.pad(26);
-    sponge_one_block<24>(s, m);  // s = expansion block 0
+    m.pad(26, cfg.xof);
+    sponge_one_block(s, m, cfg.xof);  // s = expansion block 0
   } else {
 #pragma unroll
     for (int i = 0; i < 25; ++i) s[i] = 0ull;
@@ -155,14 +155,14 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
       for (int k = 0; k < 6; ++k) carry[k] = data ? slot[(15 + k) * kHxRows + lane] : 0ull;
     }
     const bool perm = producer ? (21 * (i + 1) < nd) : (i >= 1);
-    if (perm) keccak_p<24>(s);
+    if (perm) keccak_x(s, cfg.xof);
     __syncthreads();
   }
   if (producer) {
     if (live) {
       if (bad) atomicAdd(fallback, 1u);
       xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), 1u,
-                                 cfg.proof_len, out_proof.at(r), cfg.exact_squeeze);
+                                 cfg.proof_len, out_proof.at(r), cfg.xof, cfg.exact_squeeze);
     }
     return;
   }
@@ -172,16 +172,16 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
   st64(out_part.at(r) + 8, phi);
   const uint8_t* ps = public_shares.at(r);
   uint64_t slo, shi;
-  derive_jr_seed(cfg.algo_id, ld64(ps), ld64(ps + 8), plo, phi, slo, shi);
+  derive_jr_seed(cfg.xof, cfg.algo_id, ld64(ps), ld64(ps + 8), plo, phi, slo, shi);
   st64(out_seed.at(r), slo);
   st64(out_seed.at(r) + 8, shi);
   MsgBlock m;
   m.clear();
   m.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
-  m.pad(25);
+  m.pad(25, cfg.xof);
   uint64_t s2[25];
-  sponge_one_block<24>(s2, m);
-  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r), cfg.exact_squeeze);
+  sponge_one_block(s2, m, cfg.xof);
+  squeeze_vec<FO>(s2, cfg.jr_len, out_jr.at(r), cfg.xof, cfg.exact_squeeze);
 }
 
 // Per-report weight row ("W"), element offsets (Field128 elements).
@@ -488,7 +488,7 @@ __global__ void __launch_bounds__(256) k_fpv_decide(Cfg cfg, uint32_t n, CRows l
   const uint8_t* pa = a + (size_t)cfg.verifier_len * 16u;
   const uint8_t* pb = b + (size_t)cfg.verifier_len * 16u;
   uint64_t lo, hi;
-  derive_jr_seed(cfg.algo_id, ld64(pa), ld64(pa + 8), ld64(pb), ld64(pb + 8), lo, hi);
+  derive_jr_seed(cfg.xof, cfg.algo_id, ld64(pa), ld64(pa + 8), ld64(pb), ld64(pb + 8), lo, hi);
   st64(out_msg.at(r), lo);
   st64(out_msg.at(r) + 8, hi);
 }

@@ -6,6 +6,9 @@
 // 64-bit rotations lower to two v_alignbit_b32; chi (a ^ (~b & c)) and the 3-way theta parities
 // lower to v_bitop3_b32 (gfx950).  Rounds are fully unrolled so pi is pure register renaming.
 // NR = 24 is SHAKE128 (parity with prio 0.15.1 / VDAF-07); NR = 12 is TurboSHAKE128 (VDAF-08+).
+// The kernels choose at run time (Xof below): the 12 rounds TurboSHAKE128 uses are the LAST 12 of
+// Keccak-f, so one unrolled copy of rounds 12..23 serves both and rounds 0..11 sit behind a
+// wave-uniform branch -- no second copy of the permutation in the instruction cache.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -134,13 +137,35 @@ DEVI void keccak_p(uint64_t a[25]) {
   for (int i = 0; i < 25; ++i) a[i] = ((uint64_t)h[i] << 32) | l[i];
 }
 
+// The XOF of a context: XofShake128 (Keccak-f[1600] = 24 rounds, SHAKE padding byte 0x1F; prio
+// 0.15.1 / VDAF-07, Janus 0.6) or XofTurboShake128 (Keccak-p[1600, 12], domain byte 0x01;
+// draft-irtf-cfrg-vdaf-08+).  Both absorb the same message u8(len(dst)) || dst || seed || binder.
+struct Xof {
+  uint32_t full;  // 1: 24 rounds (SHAKE128), 0: 12 rounds (TurboSHAKE128)
+  uint32_t pad;   // first padding byte: 0x1F (SHAKE128) or the TurboSHAKE domain byte 0x01
+};
+constexpr Xof kXofShake128{1u, 0x1Fu};
+constexpr Xof kXofTurboShake128{0u, 0x01u};
+
+DEVI void keccak_x(uint64_t a[25], const Xof& x) {
+  uint32_t l[25], h[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) {
+    l[i] = (uint32_t)a[i];
+    h[i] = (uint32_t)(a[i] >> 32);
+  }
+  if (x.full) keccak_rounds32<0, 12>(l, h);
+  keccak_rounds32<12, 24>(l, h);
+#pragma unroll
+  for (int i = 0; i < 25; ++i) a[i] = ((uint64_t)h[i] << 32) | l[i];
+}
+
 // ------------------------------------------------------------------------------------------------
 // XofShake128 message framing (prio src/vdaf/xof.rs; VDAF-07 §6.2.1):
 //   SHAKE128( u8(8) || dst[8] || seed[16] || binder )       rate 168 B = 21 words, pad 0x1F..0x80
 // dst = [7, 0, algo_id (u32 BE), usage (u16 BE)].
 // ------------------------------------------------------------------------------------------------
 constexpr int kRateWords = 21;
-constexpr uint8_t kShakePad = 0x1F;
 
 // Word 0 and the low byte of word 1 of every XOF message: [8, 7, 0, id BE(4), usage_hi] [usage_lo].
 DEVI uint64_t xof_word0(uint32_t algo_id, uint32_t usage) {
@@ -178,19 +203,18 @@ struct MsgBlock {
     put64(9, seed_lo);
     put64(17, seed_hi);
   }
-  // SHAKE padding for a message of `len` bytes (< 168)
-  DEVI void pad(int len) {
-    put8(len, kShakePad);
+  // sponge padding for a message of `len` bytes (< 168): the XOF's first pad byte .. 0x80
+  DEVI void pad(int len, const Xof& x) {
+    put8(len, x.pad);
     w[kRateWords - 1] ^= 0x8000000000000000ull;
   }
 };
 
 // Absorb a single padded block into a fresh state and permute.
-template <int NR = 24>
-DEVI void sponge_one_block(uint64_t s[25], const MsgBlock& m) {
+DEVI void sponge_one_block(uint64_t s[25], const MsgBlock& m, const Xof& x) {
 #pragma unroll
   for (int i = 0; i < kRateWords; ++i) s[i] = m.w[i];
 #pragma unroll
   for (int i = kRateWords; i < 25; ++i) s[i] = 0ull;
-  keccak_p<NR>(s);
+  keccak_x(s, x);
 }

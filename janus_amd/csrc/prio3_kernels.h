@@ -52,6 +52,7 @@ struct Cfg {
   uint32_t leader_share_len, helper_share_len, public_share_len, prep_share_len, prep_msg_len;
   uint32_t qr_len;          // query-randomness elements (one per gadget)
   uint32_t exact_squeeze;   // test switch: every XOF squeeze takes the per-element path
+  Xof xof;                  // XofShake128 (default) or XofTurboShake128
   const uint8_t* twiddles;  // device: alpha_m^k, k < m, Montgomery form, ES bytes each
   // FixedPointBoundedL2VecSum's second gadget, ParallelSum(PolyEval(norm poly), chunk1)
   uint32_t chunk1, calls1, m1, logm1, gp_len1;
@@ -84,7 +85,7 @@ DEVI void st64(uint8_t* p, uint64_t v) { *reinterpret_cast<uint64_t*>(p) = v; }
 // ------------------------------------------------------------------------------------------------
 // Squeeze n field elements (prio `into_field_vec`: ES-byte LE chunks, reject >= p) from a state
 // that has just been permuted after absorbing.  Accepted element i goes to out + i*ES.
-// `next(s)` produces the next rate block (keccak_p<24> for the XOF; the test kernel
+// `next(s)` produces the next rate block (keccak_x for the XOF; the test kernel
 // k_test_squeeze feeds caller-crafted blocks instead).  `exact` forces the per-element
 // rejection-sampling path for every block (PRIO3GPU_EXACT_SQUEEZE=1, a test switch).
 // ------------------------------------------------------------------------------------------------
@@ -189,33 +190,33 @@ struct SqueezeVec<Field64Ops> {
 };
 
 struct KeccakNext {
-  DEVI void operator()(uint64_t s[25]) const { keccak_p<24>(s); }
+  Xof x;
+  DEVI void operator()(uint64_t s[25]) const { keccak_x(s, x); }
 };
 
-template <class FO, int NR>
-DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out, bool exact = false) {
-  static_assert(NR == 24, "XofShake128");
-  SqueezeVec<FO>::run(s, n, out, exact, KeccakNext{});
+template <class FO>
+DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out, const Xof& x, bool exact = false) {
+  SqueezeVec<FO>::run(s, n, out, exact, KeccakNext{x});
 }
 
 // XOF(seed, dst(usage), binder=[byte]) expanded into n elements (helper share expansion).
 template <class FO>
 DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed_lo,
                                  uint64_t seed_hi, uint32_t binder_byte, uint32_t n,
-                                 uint8_t* out, bool exact) {
+                                 uint8_t* out, const Xof& x, bool exact) {
   MsgBlock m;
   m.clear();
   m.header(algo_id, usage, seed_lo, seed_hi);
   m.put8(25, binder_byte);
-  m.pad(26);
+  m.pad(26, x);
   uint64_t s[25];
-  sponge_one_block<24>(s, m);
-  squeeze_vec<FO, 24>(s, n, out, exact);
+  sponge_one_block(s, m, x);
+  squeeze_vec<FO>(s, n, out, x, exact);
 }
 
 // derive_seed(0^16, dst6, part0 || part1)   (prio Prio3::derive_joint_rand_seed)
-DEVI void derive_jr_seed(uint32_t algo_id, uint64_t p0lo, uint64_t p0hi, uint64_t p1lo,
-                         uint64_t p1hi, uint64_t& olo, uint64_t& ohi) {
+DEVI void derive_jr_seed(const Xof& x, uint32_t algo_id, uint64_t p0lo, uint64_t p0hi,
+                         uint64_t p1lo, uint64_t p1hi, uint64_t& olo, uint64_t& ohi) {
   MsgBlock m;
   m.clear();
   m.header(algo_id, DST_JOINT_RAND_SEED, 0ull, 0ull);
@@ -223,9 +224,9 @@ DEVI void derive_jr_seed(uint32_t algo_id, uint64_t p0lo, uint64_t p0hi, uint64_
   m.put64(33, p0hi);
   m.put64(41, p1lo);
   m.put64(49, p1hi);
-  m.pad(57);
+  m.pad(57, x);
   uint64_t s[25];
-  sponge_one_block<24>(s, m);
+  sponge_one_block(s, m, x);
   olo = s[0];
   ohi = s[1];
 }
@@ -244,7 +245,7 @@ DEVI uint64_t jr_data_word(int64_t g, const uint8_t* data, int64_t nd, uint64_t 
   return lo | hi;
 }
 
-DEVI void jr_part(uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t blind_hi,
+DEVI void jr_part(const Xof& x, uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t blind_hi,
                   uint64_t nonce_lo, uint64_t nonce_hi, const uint8_t* data, uint32_t nbytes,
                   uint64_t& olo, uint64_t& ohi) {
   MsgBlock pre;
@@ -258,7 +259,7 @@ DEVI void jr_part(uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t
   const int64_t total = 42 + (int64_t)nbytes;   // message bytes before padding
   const int64_t nblocks = total / 168 + 1;
   const int64_t padw = total >> 3;              // word holding the 0x1F pad byte
-  const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
+  const uint64_t padv = (uint64_t)x.pad << ((total & 7) * 8);
   uint64_t s[25];
 #pragma unroll
   for (int i = 0; i < 25; ++i) s[i] = 0ull;
@@ -293,7 +294,7 @@ DEVI void jr_part(uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t
         s[w] ^= v;
       }
     }
-    keccak_p<24>(s);
+    keccak_x(s, x);
   }
   olo = s[0];
   ohi = s[1];
@@ -317,10 +318,10 @@ __global__ void __launch_bounds__(256) k_query_rand(Cfg cfg, uint32_t n, uint64_
   m.header(cfg.algo_id, DST_QUERY_RANDOMNESS, vk_lo, vk_hi);
   m.put64(25, ld64(nz));
   m.put64(33, ld64(nz + 8));
-  m.pad(41);
+  m.pad(41, cfg.xof);
   uint64_t s[25];
-  sponge_one_block<24>(s, m);
-  squeeze_vec<FO, 24>(s, cfg.qr_len, out_t.at(r), cfg.exact_squeeze);
+  sponge_one_block(s, m, cfg.xof);
+  squeeze_vec<FO>(s, cfg.qr_len, out_t.at(r), cfg.xof, cfg.exact_squeeze);
 }
 
 // Helper share expansion: meas share XOF(k_meas, dst1, [agg_id]) and proof share
@@ -334,9 +335,9 @@ __global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t ag
   if (status && status[r] != ST_OK) return;
   const uint8_t* hs = helper_shares.at(r);
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), agg_id,
-                             cfg.proof_len, out_proof.at(r), cfg.exact_squeeze);
+                             cfg.proof_len, out_proof.at(r), cfg.xof, cfg.exact_squeeze);
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8), agg_id,
-                             cfg.meas_len, out_meas.at(r), cfg.exact_squeeze);
+                             cfg.meas_len, out_meas.at(r), cfg.xof, cfg.exact_squeeze);
 }
 
 // Joint randomness (prio prepare_init): own part over the encoded meas share, corrected seed
@@ -381,7 +382,7 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
   const int64_t total = 42 + (int64_t)nbytes;
   const int64_t nblocks = total / 168 + 1;
   const int64_t padw = total >> 3;
-  const uint64_t padv = (uint64_t)kShakePad << ((total & 7) * 8);
+  const uint64_t padv = (uint64_t)cfg.xof.pad << ((total & 7) * 8);
 
   // LDS-DMA piece q of this lane: flat piece P = 64q + lane = (row, k) with 11 pieces per row.
   // Recomputed per fill from lane = 11 la + lb (a few VALU ops per piece) instead of holding 11
@@ -493,7 +494,7 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       stage(b + 1);
     }
-    keccak_p<24>(s);
+    keccak_x(s, cfg.xof);
   }
   if (!live) return;
   const uint64_t plo = s[0], phi = s[1];
@@ -509,16 +510,16 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
     p1hi = phi;
   }
   uint64_t slo, shi;
-  derive_jr_seed(cfg.algo_id, p0lo, p0hi, p1lo, p1hi, slo, shi);
+  derive_jr_seed(cfg.xof, cfg.algo_id, p0lo, p0hi, p1lo, p1hi, slo, shi);
   st64(out_seed.at(r), slo);
   st64(out_seed.at(r) + 8, shi);
   MsgBlock m;
   m.clear();
   m.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
-  m.pad(25);
+  m.pad(25, cfg.xof);
   uint64_t s2[25];
-  sponge_one_block<24>(s2, m);
-  squeeze_vec<FO, 24>(s2, cfg.jr_len, out_jr.at(r), cfg.exact_squeeze);
+  sponge_one_block(s2, m, cfg.xof);
+  squeeze_vec<FO>(s2, cfg.jr_len, out_jr.at(r), cfg.xof, cfg.exact_squeeze);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1477,7 +1478,7 @@ __global__ void __launch_bounds__(256) k_decide(Cfg cfg, uint32_t n, CRows leade
     const uint8_t* pa = a + (size_t)cfg.verifier_len * ES;
     const uint8_t* pb = b + (size_t)cfg.verifier_len * ES;
     uint64_t lo, hi;
-    derive_jr_seed(cfg.algo_id, ld64(pa), ld64(pa + 8), ld64(pb), ld64(pb + 8), lo, hi);
+    derive_jr_seed(cfg.xof, cfg.algo_id, ld64(pa), ld64(pa + 8), ld64(pb), ld64(pb + 8), lo, hi);
     st64(out_msg.at(r), lo);
     st64(out_msg.at(r) + 8, hi);
   }
@@ -2056,9 +2057,9 @@ __global__ void __launch_bounds__(256) k_shard_jr(Cfg cfg, uint32_t n, CRows non
   const uint32_t kp = cfg.jr_len ? 64u : 32u;  // offset of k_prove in the rand row
   if (cfg.jr_len) {
     uint64_t hlo, hhi, llo, lhi;
-    jr_part(cfg.algo_id, 1, ld64(rd + 32), ld64(rd + 40), ld64(nz), ld64(nz + 8),
+    jr_part(cfg.xof, cfg.algo_id, 1, ld64(rd + 32), ld64(rd + 40), ld64(nz), ld64(nz + 8),
             helper_meas.at(r), cfg.meas_len * cfg.es, hlo, hhi);
-    jr_part(cfg.algo_id, 0, ld64(rd + 48), ld64(rd + 56), ld64(nz), ld64(nz + 8), leader.at(r),
+    jr_part(cfg.xof, cfg.algo_id, 0, ld64(rd + 48), ld64(rd + 56), ld64(nz), ld64(nz + 8), leader.at(r),
             cfg.meas_len * cfg.es, llo, lhi);
     uint8_t* p = pub.at(r);
     st64(p, llo);
@@ -2066,22 +2067,22 @@ __global__ void __launch_bounds__(256) k_shard_jr(Cfg cfg, uint32_t n, CRows non
     st64(p + 16, hlo);
     st64(p + 24, hhi);
     uint64_t slo, shi;
-    derive_jr_seed(cfg.algo_id, llo, lhi, hlo, hhi, slo, shi);
+    derive_jr_seed(cfg.xof, cfg.algo_id, llo, lhi, hlo, hhi, slo, shi);
     MsgBlock mb;
     mb.clear();
     mb.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
-    mb.pad(25);
+    mb.pad(25, cfg.xof);
     uint64_t s[25];
-    sponge_one_block<24>(s, mb);
-    squeeze_vec<FO, 24>(s, cfg.jr_len, jr_out.at(r), cfg.exact_squeeze);
+    sponge_one_block(s, mb, cfg.xof);
+    squeeze_vec<FO>(s, cfg.jr_len, jr_out.at(r), cfg.xof, cfg.exact_squeeze);
   }
   MsgBlock mb;
   mb.clear();
   mb.header(cfg.algo_id, DST_PROVE_RANDOMNESS, ld64(rd + kp), ld64(rd + kp + 8));
-  mb.pad(25);
+  mb.pad(25, cfg.xof);
   uint64_t s[25];
-  sponge_one_block<24>(s, mb);
-  squeeze_vec<FO, 24>(s, cfg.prove_rand_len, prove_rand_out.at(r), cfg.exact_squeeze);
+  sponge_one_block(s, mb, cfg.xof);
+  squeeze_vec<FO>(s, cfg.prove_rand_len, prove_rand_out.at(r), cfg.xof, cfg.exact_squeeze);
 }
 
 // leader proof share = proof - helper proof share   (thread per element)

@@ -27,6 +27,10 @@ import numpy as np
 from ._lib import Prio3GpuError, check, lib
 
 COUNT, SUM, SUMVEC, HISTOGRAM, FPVEC = 0, 1, 2, 3, 4
+# XOF behind every Prio3 stream (include/prio3gpu.h): XofShake128 = prio 0.15.1 / VDAF-07 (Janus
+# 0.6, the default); XofTurboShake128 = draft-irtf-cfrg-vdaf-08+ (forward compatibility, parity
+# unpinned)
+XOF_SHAKE128, XOF_TURBOSHAKE128 = 0, 1
 STATUS_OK, STATUS_VDAF_PREP_ERROR, STATUS_INVALID_MESSAGE = 0, 5, 8
 
 FIELD64_MODULUS = 2**64 - 2**32 + 1
@@ -199,15 +203,16 @@ class Prio3Gpu:
     """Prio3 with NUM_SHARES = 2 bound to one verify key (one Janus task) and one GPU."""
 
     def __init__(self, kind: int, verify_key: bytes, bits: int = 0, length: int = 0,
-                 chunk_length: int = 0, device: int = 0):
+                 chunk_length: int = 0, device: int = 0, xof: int = XOF_SHAKE128):
         if len(verify_key) != 16:
             raise ValueError("verify key must be 16 bytes")
         self.kind, self.bits, self.length, self.chunk_length = kind, bits, length, chunk_length
         self.verify_key = bytes(verify_key)
         self.device = device
+        self.xof = xof
         h = ctypes.c_void_p()
-        check(lib().prio3gpu_ctx_create(kind, bits, length, chunk_length, self.verify_key, device,
-                                        ctypes.byref(h)), "ctx_create")
+        check(lib().prio3gpu_ctx_create2(kind, bits, length, chunk_length, self.verify_key, device,
+                                         xof, ctypes.byref(h)), "ctx_create")
         self._ctx = h
         s = _Sizes()
         check(lib().prio3gpu_ctx_sizes(self._ctx, ctypes.byref(s)), "ctx_sizes")

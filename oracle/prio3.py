@@ -116,6 +116,77 @@ class XofShake128:
             nbytes *= 2
 
 
+# XofTurboShake128 (draft-irtf-cfrg-vdaf-08 §6.2.1; TurboSHAKE128 = RFC 9861):
+#   stream = TurboSHAKE128( u8(len(dst)) || dst || seed || binder, D = 0x01 )
+# TurboSHAKE128 = the SHAKE128 sponge (rate 168) over Keccak-p[1600, 12] -- the LAST 12 rounds of
+# Keccak-f -- with the domain byte D in place of SHAKE's 0x1F.  A pure-Python permutation (no
+# library in this image implements TurboSHAKE); pinned in tests by (a) the 24-round form of the
+# same code == hashlib.shake_128 and (b) the RFC 9861 TurboSHAKE128(M = empty, D = 0x1F) vectors.
+# Janus 0.6 runs XofShake128; this mode is forward compatibility only: PARITY UNPINNED.
+_RC = [0x0000000000000001, 0x0000000000008082, 0x800000000000808A, 0x8000000080008000,
+       0x000000000000808B, 0x0000000080000001, 0x8000000080008081, 0x8000000000008009,
+       0x000000000000008A, 0x0000000000000088, 0x0000000080008009, 0x000000008000000A,
+       0x000000008000808B, 0x800000000000008B, 0x8000000000008089, 0x8000000000008003,
+       0x8000000000008002, 0x8000000000000080, 0x000000000000800A, 0x800000008000000A,
+       0x8000000080008081, 0x8000000000008080, 0x0000000080000001, 0x8000000080008008]
+_ROT = [[0, 36, 3, 41, 18], [1, 44, 10, 45, 2], [62, 6, 43, 15, 61], [28, 55, 25, 21, 56],
+        [27, 20, 39, 8, 14]]
+_M64 = (1 << 64) - 1
+
+
+def _rotl(x: int, n: int) -> int:
+    return ((x << n) | (x >> (64 - n))) & _M64 if n else x
+
+
+def keccak_p(a: List[int], nr: int) -> List[int]:
+    """Keccak-p[1600, nr] on 25 lanes (lane x + 5y): rounds 24 - nr .. 23 of Keccak-f."""
+    for rnd in range(24 - nr, 24):
+        c = [a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20] for x in range(5)]
+        d = [c[(x - 1) % 5] ^ _rotl(c[(x + 1) % 5], 1) for x in range(5)]
+        a = [a[i] ^ d[i % 5] for i in range(25)]
+        b = [0] * 25
+        for x in range(5):
+            for y in range(5):
+                b[y + 5 * ((2 * x + 3 * y) % 5)] = _rotl(a[x + 5 * y], _ROT[x][y])
+        a = [b[i] ^ (~b[(i % 5 + 1) % 5 + 5 * (i // 5)] & b[(i % 5 + 2) % 5 + 5 * (i // 5)])
+             for i in range(25)]
+        a[0] ^= _RC[rnd]
+    return a
+
+
+def keccak_sponge(msg: bytes, pad: int, n: int, nr: int, rate: int = 168) -> bytes:
+    """Sponge over Keccak-p[1600, nr]: msg || pad || 0.. || 0x80 (pad 0x1F, nr 24 = SHAKE128;
+    pad D, nr 12 = TurboSHAKE128(msg, D))."""
+    m = bytearray(msg) + bytes([pad])
+    while len(m) % rate:
+        m.append(0)
+    m[-1] ^= 0x80
+    a = [0] * 25
+    for off in range(0, len(m), rate):
+        for i in range(rate // 8):
+            a[i] ^= int.from_bytes(m[off + 8 * i:off + 8 * i + 8], "little")
+        a = keccak_p(a, nr)
+    out = bytearray()
+    while True:
+        out += b"".join(a[i].to_bytes(8, "little") for i in range(rate // 8))
+        if len(out) >= n:
+            return bytes(out[:n])
+        a = keccak_p(a, nr)
+
+
+def turboshake128(msg: bytes, d: int, n: int) -> bytes:
+    return keccak_sponge(msg, d, n, 12)
+
+
+class XofTurboShake128(XofShake128):
+    """draft-irtf-cfrg-vdaf-08 XofTurboShake128: TurboSHAKE128(u8(len(dst)) || dst || seed ||
+    binder, D = 1).  Same message and next_vec as XofShake128."""
+    DOMAIN = 0x01
+
+    def stream(self, n: int) -> bytes:
+        return turboshake128(self.msg, self.DOMAIN, n)
+
+
 def field_vec_from_stream(fld, buf: bytes, length: int) -> Optional[List[int]]:
     """prio 0.15.1 `into_field_vec` (src/field.rs, via XofShake128::next_vec): read
     ENCODED_SIZE-byte LE chunks of the stream in order and keep those < p (rejection sampling; the
@@ -130,8 +201,8 @@ def field_vec_from_stream(fld, buf: bytes, length: int) -> Optional[List[int]]:
     return out if len(out) == length else None
 
 
-def derive_seed(seed: bytes, dst: bytes, binder: bytes) -> bytes:
-    return XofShake128(seed, dst, binder).stream(SEED_SIZE)
+def derive_seed(seed: bytes, dst: bytes, binder: bytes, xof=None) -> bytes:
+    return (xof or XofShake128)(seed, dst, binder).stream(SEED_SIZE)
 
 
 # Usage constants (prio src/vdaf/prio3.rs; VDAF-07 §7.2)
@@ -724,8 +795,11 @@ class PrepShare:
 class Prio3:
     SHARES = 2
 
-    def __init__(self, typ):
+    def __init__(self, typ, xof=None):
+        """`xof`: the XOF class (XofShake128 = prio 0.15.1 / VDAF-07, the default;
+        XofTurboShake128 = the VDAF-08+ forward-compatibility mode, parity unpinned)."""
         self.typ = typ
+        self.xof = xof or XofShake128
         self.fld = typ.Field
         self.PROOF_LEN = proof_len(typ)
         self.VERIFIER_LEN = verifier_len(typ)
@@ -786,25 +860,26 @@ class Prio3:
     # -- helpers -------------------------------------------------------------------------------
     def joint_rand_part(self, j: int, blind: bytes, meas_share, nonce: bytes) -> bytes:
         return derive_seed(blind, self.dst(DST_JOINT_RAND_PART),
-                           bytes([j]) + nonce + self.fld.encode_vec(meas_share))
+                           bytes([j]) + nonce + self.fld.encode_vec(meas_share), self.xof)
 
     def joint_rand_seed(self, parts: Sequence[bytes]) -> bytes:
-        return derive_seed(bytes(SEED_SIZE), self.dst(DST_JOINT_RAND_SEED), b"".join(parts))
+        return derive_seed(bytes(SEED_SIZE), self.dst(DST_JOINT_RAND_SEED), b"".join(parts),
+                           self.xof)
 
     def joint_rand(self, seed: bytes) -> List[int]:
-        return XofShake128(seed, self.dst(DST_JOINT_RANDOMNESS)).next_vec(
+        return self.xof(seed, self.dst(DST_JOINT_RANDOMNESS)).next_vec(
             self.fld, self.typ.JOINT_RAND_LEN)
 
     def query_rand(self, verify_key: bytes, nonce: bytes) -> List[int]:
-        return XofShake128(verify_key, self.dst(DST_QUERY_RANDOMNESS), nonce).next_vec(
+        return self.xof(verify_key, self.dst(DST_QUERY_RANDOMNESS), nonce).next_vec(
             self.fld, self.typ.QUERY_RAND_LEN)
 
     def expand_meas_share(self, seed: bytes, j: int) -> List[int]:
-        return XofShake128(seed, self.dst(DST_MEASUREMENT_SHARE), bytes([j])).next_vec(
+        return self.xof(seed, self.dst(DST_MEASUREMENT_SHARE), bytes([j])).next_vec(
             self.fld, self.typ.MEAS_LEN)
 
     def expand_proof_share(self, seed: bytes, j: int) -> List[int]:
-        return XofShake128(seed, self.dst(DST_PROOF_SHARE), bytes([j])).next_vec(
+        return self.xof(seed, self.dst(DST_PROOF_SHARE), bytes([j])).next_vec(
             self.fld, self.PROOF_LEN)
 
     # -- Client::shard (prio `shard_with_random`) ------------------------------------------------
@@ -834,7 +909,7 @@ class Prio3:
             public_parts = [self.joint_rand_part(0, leader_blind, leader_meas, nonce)] + parts
             joint_rand = self.joint_rand(self.joint_rand_seed(public_parts))
         k_prove = next(it)
-        prove_rand = XofShake128(k_prove, self.dst(DST_PROVE_RANDOMNESS)).next_vec(
+        prove_rand = self.xof(k_prove, self.dst(DST_PROVE_RANDOMNESS)).next_vec(
             self.fld, self.typ.PROVE_RAND_LEN)
         proof = flp_prove(self.typ, encoded, prove_rand, joint_rand)
         leader_proof = list(proof)

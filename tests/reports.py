@@ -66,9 +66,12 @@ def _pack(rows: List[bytes], width: int) -> np.ndarray:
     return np.frombuffer(b"".join(rows), dtype=np.uint8).reshape(len(rows), width).copy()
 
 
-def make_batch(name: str, n: int, cfg_id: bytes = None, start: int = 0) -> Batch:
+def make_batch(name: str, n: int, cfg_id: bytes = None, start: int = 0, xof=None) -> Batch:
+    """`xof`: oracle XOF class (default XofShake128; O.XofTurboShake128 for the VDAF-08+ mode)."""
     cfg = CONFIGS[name]
     v = cfg["ctor"]()
+    if xof is not None:
+        v.xof = xof
     cfg_id = cfg_id if cfg_id is not None else name.encode()
     vk = O.synth_verify_key(cfg_id)
     keys = ["public_share", "leader_input_share", "helper_input_share", "leader_prep_share",

@@ -165,3 +165,38 @@ def test_noncanonical_decode_rejected():
     raw[:16] = b"\xff" * 16
     with pytest.raises(ValueError):
         b.vdaf.decode_input_share(0, bytes(raw))
+
+
+# ---- XofTurboShake128 (VDAF-08+ forward-compatibility mode; parity unpinned) ---------------------
+
+def test_keccak_sponge_24_rounds_is_shake128():
+    """The pure-Python Keccak-p behind the TurboSHAKE oracle, run with 24 rounds and SHAKE's pad
+    byte, is hashlib's SHAKE128 (FIPS 202) -- multi-block absorb and squeeze included."""
+    import hashlib
+    from oracle.prio3 import keccak_sponge
+    for msg in (b"", b"abc", bytes(range(167)), bytes(range(168)), bytes(500)):
+        assert keccak_sponge(msg, 0x1F, 400, 24) == hashlib.shake_128(msg).digest(400)
+
+
+def test_turboshake128_rfc9861_vectors():
+    """RFC 9861 TurboSHAKE128(M = empty, D = 0x1F): 32- and 64-byte outputs."""
+    from oracle.prio3 import turboshake128
+    v32 = bytes.fromhex("1e415f1c5983aff2169217277d17bb538cd945a397ddec541f1ce41af2c1b74c")
+    v64 = v32 + bytes.fromhex("3e8ccae2a4dae56c84a04c2385c03c15e8193bdf58737363321691c05462c8df")
+    assert turboshake128(b"", 0x1F, 32) == v32
+    assert turboshake128(b"", 0x1F, 64) == v64
+
+
+@pytest.mark.parametrize("name", ["count", "sum8", "sumvec_small", "hist4"])
+def test_turboshake_mode_round_trip(name):
+    """Prio3 over XofTurboShake128: the transcript differs from XofShake128's, every report
+    verifies, and unshard(aggregate) == plaintext sum."""
+    from oracle import prio3 as O
+    from tests.reports import make_batch, plaintext_sum
+    bt = make_batch(name, 4, xof=O.XofTurboShake128)
+    bs = make_batch(name, 4)
+    assert (bt.leader_prep != bs.leader_prep).any()
+    v = bt.vdaf
+    agg_l = v.aggregate([v.fld.decode_vec(bt.leader_out[r].tobytes()) for r in range(bt.n)])
+    agg_h = v.aggregate([v.fld.decode_vec(bt.helper_out[r].tobytes()) for r in range(bt.n)])
+    assert v.unshard([agg_l, agg_h]) == plaintext_sum(bt)
