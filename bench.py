@@ -144,7 +144,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: the host CPUs this process may use)")
     ap.add_argument("--overlap", type=int, default=0,
-                    help="leader and helper on separate contexts/streams, prepare_init concurrent")
+                    help="1: leader and helper on separate contexts/streams, prepare_init "
+                         "concurrent; 2: pipelined schedule (each batch's HBM-bound FLP query "
+                         "under the other aggregator's Keccak, async contexts, see DESIGN §5)")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -307,6 +309,63 @@ def main():
 
     pool = ThreadPoolExecutor(max_workers=W) if W > 1 else None
 
+    # --overlap 2: the pipelined schedule.  Two async contexts (leader A, helper B), two leader
+    # states (step i+1's XOF phase runs before step i's prepare_next).  Per step i:
+    #   B waits A; B: helper XOF(i); mark mB          | A: leader query(i) (HBM) under it; mark mA
+    #   A waits mB; A: leader XOF(i+1)                | B: helper query(i) (HBM) under it
+    #   B waits mA; B: decide(i), prepare_next + accumulate(i), report meta; mark mB2
+    #   A waits mB2; A: leader prepare_next + accumulate(i), report meta
+    # Both streams are drained (and, N > 1, the partials merged) at the end of the run.
+    pipe = None
+    if args.overlap == 2:
+        assert W == 1, "--overlap 2 runs one job worker"
+        wk = workers[0]
+        A, Bv = wk.v, wk.hv
+        A.set_async(True)
+        Bv.set_async(True)
+        pipe = dict(ls=[wk.ls, wk.v.new_state(0, wk.n)],
+                    lst=[d_lst, torch.zeros(B, dtype=torch.uint8, device=dev)])
+
+    def run_pipelined(k_steps):
+        wk, p = workers[0], workers[0].p
+        A, Bv = wk.v, wk.hv
+        ls, lst = pipe["ls"], pipe["lst"]
+        xof = lambda v, st, status, inp: check(L.prio3gpu_prepare_init_xof(
+            v._ctx, st._h, wk.n, p["nonces"], p["pub"], inp, P(status)), "prepare_init_xof")
+        query = lambda v, st, status, out: check(L.prio3gpu_prepare_init_query(
+            v._ctx, st._h, wk.n, out, P(status)), "prepare_init_query")
+        xof(A, ls[0], lst[0], p["lin"])
+        for i in range(k_steps):
+            cur, nxt = i % 2, (i + 1) % 2
+            Bv.wait_for(A)
+            xof(Bv, wk.hs, d_hst, p["hin"])
+            mB = Bv.mark()
+            query(A, ls[cur], lst[cur], p["lprep"])
+            mA = A.mark()
+            if i + 1 < k_steps:
+                A.wait_for(Bv, mB)
+                xof(A, ls[nxt], lst[nxt], p["lin"])
+            query(Bv, wk.hs, d_hst, P(d_hprep2))
+            Bv.wait_for(A, mA)
+            check(L.prio3gpu_prepare_shares_to_prepare_message(Bv._ctx, wk.n, p["lprep"],
+                                                               P(d_hprep2), p["msgs"], p["hst"]),
+                  "decide")
+            check(L.prio3gpu_prepare_next(Bv._ctx, wk.hs._h, wk.n, p["msgs"], p["hst"], None,
+                                          None, wk.hpart._h), "helper prepare_next")
+            check(L.prio3gpu_agg_update_reports(wk.hpart._h, wk.n, p["nonces"], p["times"],
+                                                p["hst"], None), "helper report checksums")
+            mB2 = Bv.mark()
+            A.wait_for(Bv, mB2)
+            check(L.prio3gpu_prepare_next(A._ctx, ls[cur]._h, wk.n, p["msgs"], P(lst[cur]), None,
+                                          None, wk.lpart._h), "leader prepare_next")
+            check(L.prio3gpu_agg_update_reports(wk.lpart._h, wk.n, p["nonces"], p["times"],
+                                                P(lst[cur]), None), "leader report checksums")
+        A.sync()
+        Bv.sync()
+        if comm is not None:
+            comm.allreduce(A, wk.lpart, wk.lagg)
+            comm.allreduce(Bv, wk.hpart, wk.hagg)
+
     def step():
         d_lst.zero_()
         d_hst.zero_()
@@ -320,8 +379,13 @@ def main():
                 comm.allreduce(wk.v, wk.lpart, wk.lagg)
                 comm.allreduce(wk.hv, wk.hpart, wk.hagg)
 
-    for _ in range(args.warmup):
-        step()
+    d_hprep2 = (torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
+                if args.overlap == 2 else None)
+    if pipe is not None:
+        run_pipelined(max(1, args.warmup))
+    else:
+        for _ in range(args.warmup):
+            step()
     ctxs = []
     for wk in workers:
         ctxs += [wk.v._ctx] + ([wk.hv._ctx] if wk.hv is not wk.v else [])
@@ -337,8 +401,11 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    if pipe is not None:
+        run_pipelined(args.steps)
+    else:
+        for _ in range(args.steps):
+            step()
     barrier()
     elapsed = time.perf_counter() - t0
     kt = {}
@@ -359,7 +426,11 @@ def main():
 
     # ---- parity gate: statuses, counts, aggregate == plaintext sum (and == CPU restatement) ------
     assert int(d_lst.max().item()) == 0 and int(d_hst.max().item()) == 0, "rejected reports"
-    total_steps = args.warmup + args.steps
+    total_steps = (max(1, args.warmup) if pipe is not None else args.warmup) + args.steps
+    if pipe is not None:
+        assert int(pipe["lst"][1].max().item()) == 0, "rejected reports"
+        for v_ in (workers[0].v, workers[0].hv):
+            v_.set_async(False)
     def total(attr):  # merge the workers' aggregates (mod p) and counts
         acc, cnt = None, 0
         for wk in workers:

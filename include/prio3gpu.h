@@ -127,6 +127,18 @@ int prio3gpu_ctx_destroy(prio3gpu_ctx* ctx);
 int prio3gpu_ctx_sizes(const prio3gpu_ctx* ctx, prio3gpu_sizes* out);
 /* Wait for all work queued on the context's stream. */
 int prio3gpu_ctx_sync(prio3gpu_ctx* ctx);
+/* Async mode (default off): a call whose buffers are ALL device memory returns once its work is
+ * queued on the context's stream instead of waiting for it (calls with any host buffer still
+ * wait: their staging copies / results need it).  Lets a job driver queue job k+1 behind job k
+ * (Janus runs aggregation jobs concurrently, aggregator/src/binary_utils/job_driver.rs:119-216);
+ * order work across contexts with prio3gpu_ctx_wait and finish with prio3gpu_ctx_sync. */
+int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
+/* Work queued on `ctx` from now on starts only after all work queued on `other` so far. */
+int prio3gpu_ctx_wait(prio3gpu_ctx* ctx, prio3gpu_ctx* other);
+/* The same in two steps: mark what is queued on `ctx` now; later make another context wait for
+ * that mark.  Marks live in a ring of 16 per context: wait on a mark before 16 newer ones. */
+int prio3gpu_ctx_mark(prio3gpu_ctx* ctx, int* out_mark);
+int prio3gpu_ctx_wait_mark(prio3gpu_ctx* ctx, prio3gpu_ctx* other, int mark);
 /* The context's HIP stream (hipStream_t), for callers that interoperate (e.g. bench timing). */
 void* prio3gpu_ctx_stream(prio3gpu_ctx* ctx);
 
@@ -176,6 +188,16 @@ int prio3gpu_unshard(const prio3gpu_ctx* ctx, const uint8_t* agg_shares, size_t 
 int prio3gpu_prepare_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const uint8_t* nonces,
                           const uint8_t* public_shares, const uint8_t* input_shares,
                           uint8_t* out_prep_shares, uint8_t* status);
+/* prio3gpu_prepare_init in two phases over the same state and n: the XOF phase (query and joint
+ * randomness, the helper's share expansion; VALU-bound Keccak) and the FLP-query phase (weights +
+ * one HBM pass over the measurement shares).  prepare_init == xof then query.  Split so a driver
+ * can overlap one batch's HBM-bound query with another batch's Keccak on a second context.  The
+ * input buffers must stay valid until the query phase. */
+int prio3gpu_prepare_init_xof(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n,
+                              const uint8_t* nonces, const uint8_t* public_shares,
+                              const uint8_t* input_shares, uint8_t* status);
+int prio3gpu_prepare_init_query(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n,
+                                uint8_t* out_prep_shares, uint8_t* status);
 
 /* prepare_shares_to_prepare_message for n reports (leader share, helper share) -> prep msg. */
 int prio3gpu_prepare_shares_to_prepare_message(prio3gpu_ctx* ctx, size_t n,

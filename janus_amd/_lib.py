@@ -67,6 +67,12 @@ def _declare(lib):
         "prio3gpu_ctx_create2": (c.c_int, [c.c_int, c.c_uint32, c.c_uint32, c.c_uint32,
                                            c.c_char_p, c.c_int, c.c_int, c.POINTER(P)]),
         "prio3gpu_ctx_destroy": (c.c_int, [P]),
+        "prio3gpu_ctx_set_async": (c.c_int, [P, c.c_int]),
+        "prio3gpu_ctx_wait": (c.c_int, [P, P]),
+        "prio3gpu_ctx_mark": (c.c_int, [P, c.POINTER(c.c_int)]),
+        "prio3gpu_ctx_wait_mark": (c.c_int, [P, P, c.c_int]),
+        "prio3gpu_prepare_init_xof": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, u8p]),
+        "prio3gpu_prepare_init_query": (c.c_int, [P, P, c.c_size_t, u8p, u8p]),
         "prio3gpu_ctx_sizes": (c.c_int, [P, P]),
         "prio3gpu_ctx_sync": (c.c_int, [P]),
         "prio3gpu_ctx_stream": (P, [P]),
@@ -144,7 +150,9 @@ def _declare(lib):
 # Every symbol include/prio3gpu.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "prio3gpu_ctx_create", "prio3gpu_ctx_create2", "prio3gpu_ctx_destroy", "prio3gpu_ctx_sizes",
-    "prio3gpu_ctx_sync",
+    "prio3gpu_ctx_sync", "prio3gpu_ctx_set_async", "prio3gpu_ctx_wait", "prio3gpu_ctx_mark",
+    "prio3gpu_ctx_wait_mark",
+    "prio3gpu_prepare_init_xof", "prio3gpu_prepare_init_query",
     "prio3gpu_ctx_stream", "prio3gpu_state_create", "prio3gpu_state_destroy",
     "prio3gpu_agg_create", "prio3gpu_agg_destroy", "prio3gpu_agg_reset", "prio3gpu_agg_read",
     "prio3gpu_agg_merge_bytes", "prio3gpu_agg_update_reports", "prio3gpu_agg_read_reports",

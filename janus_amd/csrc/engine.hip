@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <initializer_list>
 #include <vector>
 
 #include "../../include/prio3gpu.h"
@@ -190,6 +191,19 @@ struct prio3gpu_ctx {
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
+  // async mode (prio3gpu_ctx_set_async): calls whose buffers are all device memory return once
+  // their work is queued; cross-context order via prio3gpu_ctx_wait
+  bool async_mode = false;
+  static constexpr int kMarks = 16;
+  hipEvent_t ev[kMarks] = {};  // ring of marks (prio3gpu_ctx_mark)
+  int ev_next = 0;
+  // the device-side accumulation plan of the last call (single slot, no per-report slots):
+  // reused while (n, speculative layout, slot count) are unchanged -- no host planning, no upload
+  bool plan_valid = false;
+  size_t plan_n = 0;
+  uint32_t plan_slots = 0, plan_nd = 0, plan_e0 = 0, plan_e1 = 0;
+  bool plan_spec = false;
+  uint32_t plan_ndir = 0, plan_nspec = 0, plan_nch = 0, plan_tiles = 0, plan_epb = 0;
 };
 
 namespace {
@@ -222,6 +236,8 @@ struct prio3gpu_state {
   DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input, w;
   DevBuf fpart, flags;  // FixedPointBoundedL2VecSum: wire partials per row group, query flags
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
+  CRows proof_rows{nullptr, 0};  // proof shares (prepare_init_xof -> prepare_init_query)
+  bool xof_done = false;         // the XOF phase ran; the query phase is due
   // speculative accumulation: per-wave column sums of meas-share words, written by k_jr
   DevBuf spec_lo, spec_cy;
   bool spec_ok = false;
@@ -537,8 +553,12 @@ int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, 
 }
 
 template <class FO>
-int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
-                        const uint8_t* d_pub, const uint8_t* d_in, uint8_t* d_status) {
+int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_status);
+
+// prepare_init, first phase: query randomness, (helper) share expansion, joint randomness.
+template <class FO>
+int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
+                    const uint8_t* d_pub, const uint8_t* d_in, uint8_t* d_status) {
   const Cfg& g = c->cfg;
   const uint32_t es = g.es;
   const uint32_t N = (uint32_t)n;
@@ -585,10 +605,10 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
     }
     if (fused_done) {
       st->spec_ok = false;
-      CHK(launch_fpv_query(c, st, n, CRows{mo.base, mo.stride}, CRows{po.base, po.stride},
-                           d_status));
       st->meas_rows = CRows{mo.base, mo.stride};
+      st->proof_rows = CRows{po.base, po.stride};
       st->n = n;
+      st->xof_done = true;
       return 0;
     }
     {
@@ -626,11 +646,29 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
                          spec_lo, spec_cy);
     }
   }
+  HIPCHK(hipGetLastError());
+  st->meas_rows = meas;
+  st->proof_rows = proof;
+  st->n = n;
+  st->xof_done = true;
+  return 0;
+}
+
+// prepare_init, second phase: the FLP query over the shares the first phase left in the state.
+template <class FO>
+int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  const uint32_t es = g.es;
+  const uint32_t N = (uint32_t)n;
+  const CRows meas = st->meas_rows, proof = st->proof_rows;
+  if (!st->xof_done || st->n != n) {
+    set_err("prepare_init query phase without its XOF phase over the same %zu reports", n);
+    return PRIO3GPU_E_ARG;
+  }
+  st->xof_done = false;
   if constexpr (FO::ES == 16) {
     if (g.kind == KIND_FPVEC) {
       CHK(launch_fpv_query(c, st, n, meas, proof, d_status));
-      st->meas_rows = meas;
-      st->n = n;
       return 0;
     }
   }
@@ -701,9 +739,14 @@ int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uin
                        Rows{st->prep.u8(), g.prep_share_len}, d_status);
   }
   HIPCHK(hipGetLastError());
-  st->meas_rows = meas;
-  st->n = n;
   return 0;
+}
+
+template <class FO>
+int launch_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
+                        const uint8_t* d_pub, const uint8_t* d_in, uint8_t* d_status) {
+  CHK(launch_prep_xof<FO>(c, st, n, d_nonces, d_pub, d_in, d_status));
+  return launch_prep_query<FO>(c, st, n, d_status);
 }
 
 template <class FO>
@@ -733,105 +776,133 @@ template <class FO>
 int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint32_t* slots,
                       const uint8_t* d_status, prio3gpu_agg* agg) {
   const Cfg& g = c->cfg;
-  std::vector<uint32_t> hslots;
-  const uint32_t* sl = slots;
-  if (slots && is_device_ptr(slots)) {
-    hslots.resize(n);
-    HIPCHK(hipMemcpyAsync(hslots.data(), slots, n * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    sl = hslots.data();
-  }
   const uint32_t S = agg->slots;
-  for (size_t r = 0; r < n; ++r) {
-    const uint32_t s = sl ? sl[r] : 0;
-    if (s >= S) {
-      set_err("batch slot %u out of range (%u slots)", s, S);
-      return PRIO3GPU_E_ARG;
-    }
-  }
-  auto slot_of = [&](size_t r) -> uint32_t { return sl ? sl[r] : 0u; };
-  // Chunks (runs of reports of one slot, contiguous per slot in chunk order) of two kinds:
-  //  * direct: k_accum_partial sums every measurement element of the chunk's reports;
-  //  * speculative (whole waves of 64 reports whose slots agree, when k_jr left column sums):
-  //    k_accum_spec folds the per-wave sums of elements [e0, e1) and corrects the rejected rows,
-  //    k_accum_partial adds the few edge elements outside that range.
   const bool spec = st->spec_ok && st->spec_n == n && FO::ES == 16;
-  const size_t nw = (n + 63) / 64;
-  std::vector<std::vector<uint32_t>> spec_w(S), direct_r(S);
-  if (spec) {
-    for (size_t w = 0; w < nw; ++w) {
-      const size_t r0 = 64 * w, r1 = std::min(n, r0 + 64);
-      const uint32_t s = slot_of(r0);
-      bool uni = true;
-      for (size_t r = r0 + 1; r < r1 && uni; ++r) uni = slot_of(r) == s;
-      if (uni) {
-        spec_w[s].push_back((uint32_t)w);
-      } else {
-        for (size_t r = r0; r < r1; ++r) direct_r[slot_of(r)].push_back((uint32_t)r);
-      }
-    }
-  } else {
-    for (size_t r = 0; r < n; ++r) direct_r[slot_of(r)].push_back((uint32_t)r);
-  }
   const uint32_t epb = std::min<uint32_t>(256, std::max<uint32_t>(1, g.meas_len));
-  const uint32_t G = 256 / epb;
   const uint32_t tiles = (g.meas_len + epb - 1) / epb;
-  const size_t target_chunks = std::max<size_t>(1, 2048 / tiles);
-  const size_t CH = std::max<size_t>((size_t)G * 4, (n + target_chunks - 1) / target_chunks);
-  const size_t WCH = 32;  // waves per speculative chunk
-  auto& perm = c->h_perm;
-  auto& cb = c->h_chunk_begin;
-  auto& cs = c->h_chunk_slot;
-  perm.clear();
-  cb.clear();
-  cs.clear();
-  std::vector<uint32_t> dir_ids, spec_ids, swb, wl;
-  for (uint32_t s = 0; s < S; ++s) {
-    const auto& sw = spec_w[s];
-    for (size_t i = 0; i < sw.size(); i += WCH) {
-      spec_ids.push_back((uint32_t)cs.size());
-      cb.push_back((uint32_t)perm.size());
-      cs.push_back(s);
-      swb.push_back((uint32_t)wl.size());
-      for (size_t q = i; q < std::min(sw.size(), i + WCH); ++q) {
-        wl.push_back(sw[q]);
-        for (size_t r = 64 * (size_t)sw[q]; r < std::min(n, 64 * (size_t)sw[q] + 64); ++r)
-          perm.push_back((uint32_t)r);
+  // One batch slot and the same batch shape as the last call: the plan on the device still holds
+  // (no host planning, no upload, no stream synchronisation).
+  const bool reuse = !slots && c->plan_valid && c->plan_n == n && c->plan_slots == S &&
+                     c->plan_spec == spec &&
+                     (!spec || (c->plan_nd == st->spec_nd && c->plan_e0 == st->spec_e0 &&
+                                c->plan_e1 == st->spec_e1));
+  if (!reuse) {
+    c->plan_valid = false;
+    std::vector<uint32_t> hslots;
+    const uint32_t* sl = slots;
+    if (slots && is_device_ptr(slots)) {
+      hslots.resize(n);
+      HIPCHK(hipMemcpyAsync(hslots.data(), slots, n * 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));
+      sl = hslots.data();
+    }
+    for (size_t r = 0; r < n; ++r) {
+      const uint32_t s = sl ? sl[r] : 0;
+      if (s >= S) {
+        set_err("batch slot %u out of range (%u slots)", s, S);
+        return PRIO3GPU_E_ARG;
       }
     }
-    const auto& dr = direct_r[s];
-    for (size_t i = 0; i < dr.size(); i += CH) {
-      dir_ids.push_back((uint32_t)cs.size());
-      cb.push_back((uint32_t)perm.size());
-      cs.push_back(s);
-      perm.insert(perm.end(), dr.begin() + i, dr.begin() + std::min(dr.size(), i + CH));
+    auto slot_of = [&](size_t r) -> uint32_t { return sl ? sl[r] : 0u; };
+    // Chunks (runs of reports of one slot, contiguous per slot in chunk order) of two kinds:
+    //  * direct: k_accum_partial sums every measurement element of the chunk's reports;
+    //  * speculative (whole waves of 64 reports whose slots agree, when k_jr left column sums):
+    //    k_accum_spec folds the per-wave sums of elements [e0, e1) and corrects the rejected
+    //    rows, k_accum_partial adds the few edge elements outside that range.
+    const size_t nw = (n + 63) / 64;
+    std::vector<std::vector<uint32_t>> spec_w(S), direct_r(S);
+    if (spec) {
+      for (size_t w = 0; w < nw; ++w) {
+        const size_t r0 = 64 * w, r1 = std::min(n, r0 + 64);
+        const uint32_t s = slot_of(r0);
+        bool uni = true;
+        for (size_t r = r0 + 1; r < r1 && uni; ++r) uni = slot_of(r) == s;
+        if (uni) {
+          spec_w[s].push_back((uint32_t)w);
+        } else {
+          for (size_t r = r0; r < r1; ++r) direct_r[slot_of(r)].push_back((uint32_t)r);
+        }
+      }
+    } else {
+      for (size_t r = 0; r < n; ++r) direct_r[slot_of(r)].push_back((uint32_t)r);
     }
+    const uint32_t G = 256 / epb;
+    const size_t target_chunks = std::max<size_t>(1, 2048 / tiles);
+    const size_t CH = std::max<size_t>((size_t)G * 4, (n + target_chunks - 1) / target_chunks);
+    const size_t WCH = 32;  // waves per speculative chunk
+    auto& perm = c->h_perm;
+    auto& cb = c->h_chunk_begin;
+    auto& cs = c->h_chunk_slot;
+    perm.clear();
+    cb.clear();
+    cs.clear();
+    std::vector<uint32_t> dir_ids, spec_ids, swb, wl;
+    for (uint32_t s = 0; s < S; ++s) {
+      const auto& sw = spec_w[s];
+      for (size_t i = 0; i < sw.size(); i += WCH) {
+        spec_ids.push_back((uint32_t)cs.size());
+        cb.push_back((uint32_t)perm.size());
+        cs.push_back(s);
+        swb.push_back((uint32_t)wl.size());
+        for (size_t q = i; q < std::min(sw.size(), i + WCH); ++q) {
+          wl.push_back(sw[q]);
+          for (size_t r = 64 * (size_t)sw[q]; r < std::min(n, 64 * (size_t)sw[q] + 64); ++r)
+            perm.push_back((uint32_t)r);
+        }
+      }
+      const auto& dr = direct_r[s];
+      for (size_t i = 0; i < dr.size(); i += CH) {
+        dir_ids.push_back((uint32_t)cs.size());
+        cb.push_back((uint32_t)perm.size());
+        cs.push_back(s);
+        perm.insert(perm.end(), dr.begin() + i, dr.begin() + std::min(dr.size(), i + CH));
+      }
+    }
+    const uint32_t nch = (uint32_t)cs.size();
+    if (nch == 0) return 0;
+    cb.push_back((uint32_t)perm.size());
+    swb.push_back((uint32_t)wl.size());
+    const uint32_t ndir = (uint32_t)dir_ids.size(), nspec = (uint32_t)spec_ids.size();
+    CHK(c->perm.ensure(std::max<size_t>(1, perm.size()) * 4));
+    CHK(c->chunks.ensure((size_t)(2 * nch + 1) * 4));
+    CHK(c->partials.ensure((size_t)nch * g.meas_len * g.es));
+    CHK(c->pcounts.ensure((size_t)nch * 4));
+    CHK(c->spec_idx.ensure((size_t)(ndir + 2 * nspec + 1 + wl.size() + 1) * 4));
+    HIPCHK(hipMemcpyAsync(c->perm.p, perm.data(), perm.size() * 4, hipMemcpyHostToDevice, c->stream));
+    uint32_t* d_cb = reinterpret_cast<uint32_t*>(c->chunks.p);
+    uint32_t* d_cs = d_cb + nch + 1;
+    HIPCHK(hipMemcpyAsync(d_cb, cb.data(), (nch + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d_cs, cs.data(), nch * 4, hipMemcpyHostToDevice, c->stream));
+    uint32_t* d_dir = reinterpret_cast<uint32_t*>(c->spec_idx.p);
+    uint32_t* d_sid = d_dir + ndir;
+    uint32_t* d_swb = d_sid + nspec;
+    uint32_t* d_wl = d_swb + nspec + 1;
+    if (ndir) HIPCHK(hipMemcpyAsync(d_dir, dir_ids.data(), ndir * 4, hipMemcpyHostToDevice, c->stream));
+    if (nspec) {
+      HIPCHK(hipMemcpyAsync(d_sid, spec_ids.data(), nspec * 4, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(d_swb, swb.data(), (nspec + 1) * 4, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemcpyAsync(d_wl, wl.data(), wl.size() * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    // the host vectors must outlive the async copies (and a later re-plan rewrites them)
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->plan_ndir = ndir;
+    c->plan_nspec = nspec;
+    c->plan_nch = nch;
+    c->plan_valid = !slots;
+    c->plan_n = n;
+    c->plan_slots = S;
+    c->plan_spec = spec;
+    c->plan_nd = st->spec_nd;
+    c->plan_e0 = st->spec_e0;
+    c->plan_e1 = st->spec_e1;
   }
-  const uint32_t nch = (uint32_t)cs.size();
-  if (nch == 0) return 0;
-  cb.push_back((uint32_t)perm.size());
-  swb.push_back((uint32_t)wl.size());
-  const uint32_t ndir = (uint32_t)dir_ids.size(), nspec = (uint32_t)spec_ids.size();
-  CHK(c->perm.ensure(std::max<size_t>(1, perm.size()) * 4));
-  CHK(c->chunks.ensure((size_t)(2 * nch + 1) * 4));
-  CHK(c->partials.ensure((size_t)nch * g.meas_len * g.es));
-  CHK(c->pcounts.ensure((size_t)nch * 4));
-  CHK(c->spec_idx.ensure((size_t)(ndir + 2 * nspec + 1 + wl.size() + 1) * 4));
-  HIPCHK(hipMemcpyAsync(c->perm.p, perm.data(), perm.size() * 4, hipMemcpyHostToDevice, c->stream));
-  uint32_t* d_cb = reinterpret_cast<uint32_t*>(c->chunks.p);
-  uint32_t* d_cs = d_cb + nch + 1;
-  HIPCHK(hipMemcpyAsync(d_cb, cb.data(), (nch + 1) * 4, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(d_cs, cs.data(), nch * 4, hipMemcpyHostToDevice, c->stream));
-  uint32_t* d_dir = reinterpret_cast<uint32_t*>(c->spec_idx.p);
-  uint32_t* d_sid = d_dir + ndir;
-  uint32_t* d_swb = d_sid + nspec;
-  uint32_t* d_wl = d_swb + nspec + 1;
-  if (ndir) HIPCHK(hipMemcpyAsync(d_dir, dir_ids.data(), ndir * 4, hipMemcpyHostToDevice, c->stream));
-  if (nspec) {
-    HIPCHK(hipMemcpyAsync(d_sid, spec_ids.data(), nspec * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(d_swb, swb.data(), (nspec + 1) * 4, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(d_wl, wl.data(), wl.size() * 4, hipMemcpyHostToDevice, c->stream));
-  }
+  const uint32_t ndir = c->plan_ndir, nspec = c->plan_nspec, nch = c->plan_nch;
+  const uint32_t* d_cb = reinterpret_cast<const uint32_t*>(c->chunks.p);
+  const uint32_t* d_cs = d_cb + nch + 1;
+  const uint32_t* d_dir = reinterpret_cast<const uint32_t*>(c->spec_idx.p);
+  const uint32_t* d_sid = d_dir + ndir;
+  const uint32_t* d_swb = d_sid + nspec;
+  const uint32_t* d_wl = d_swb + nspec + 1;
   const uint32_t* d_perm = reinterpret_cast<const uint32_t*>(c->perm.p);
   uint32_t* d_pc = reinterpret_cast<uint32_t*>(c->pcounts.p);
   const size_t red_lds = 256 * sizeof(typename FO::T) + 16;
@@ -869,8 +940,6 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
                        agg->share.u8(), reinterpret_cast<unsigned long long*>(agg->counts.p));
   }
   HIPCHK(hipGetLastError());
-  // The host vectors must outlive the async copies.
-  HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
 
@@ -936,6 +1005,17 @@ int stage_status(prio3gpu_ctx* c, DevBuf& buf, uint8_t* status, size_t n, uint8_
   CHK(buf.ensure(n));
   HIPCHK(hipMemcpyAsync(buf.p, status, n, hipMemcpyHostToDevice, c->stream));
   *d_status = buf.u8();
+  return 0;
+}
+
+// End of an ABI call: wait for the context's stream unless the context is in async mode and every
+// buffer the call touched is device memory (host inputs are staged by async copies and host
+// outputs are written by them: those need the wait).
+int finish_call(prio3gpu_ctx* c, std::initializer_list<const void*> bufs) {
+  bool host = !c->async_mode;
+  for (const void* b : bufs)
+    if (b && !is_device_ptr(b)) host = true;
+  if (host) HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
 
@@ -1016,6 +1096,8 @@ int prio3gpu_ctx_destroy(prio3gpu_ctx* c) {
     (void)hipEventDestroy(r.b);
   }
   for (auto ev : c->prof.pool) (void)hipEventDestroy(ev);
+  for (auto ev : c->ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -1304,8 +1386,90 @@ int prio3gpu_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const u
     CHK(launch_prepare_init<Field128Ops>(c, st, n, d_nonces, d_pub, d_in, d_status));
   CHK(copy_out(c, out_prep_shares, st->prep.p, n * g.prep_share_len));
   CHK(copy_out(c, status, d_status, n));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  return finish_call(c, {nonces, public_shares, input_shares, out_prep_shares, status});
+}
+
+int prio3gpu_prepare_init_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* nonces,
+                              const uint8_t* public_shares, const uint8_t* input_shares,
+                              uint8_t* status) {
+  CHK(check_state(c, st, n));
+  if (n == 0) return 0;
+  if (!nonces || !input_shares || (c->cfg.jr_len && !public_shares)) {
+    set_err("null input");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const Cfg& g = c->cfg;
+  const uint8_t *d_nonces, *d_pub, *d_in;
+  CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));
+  CHK(stage_in(c, st->pub, public_shares, n * g.public_share_len, &d_pub));
+  const size_t in_len = st->agg_id == 0 ? g.leader_share_len : g.helper_share_len;
+  CHK(stage_in(c, st->input, input_shares, n * in_len, &d_in));
+  uint8_t* d_status;
+  CHK(stage_status(c, st->status, status, n, &d_status));
+  if (is_f64(c))
+    CHK(launch_prep_xof<Field64Ops>(c, st, n, d_nonces, d_pub, d_in, d_status));
+  else
+    CHK(launch_prep_xof<Field128Ops>(c, st, n, d_nonces, d_pub, d_in, d_status));
+  CHK(copy_out(c, status, d_status, n));
+  return finish_call(c, {nonces, public_shares, input_shares, status});
+}
+
+int prio3gpu_prepare_init_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n,
+                                uint8_t* out_prep_shares, uint8_t* status) {
+  CHK(check_state(c, st, n));
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  uint8_t* d_status;
+  CHK(stage_status(c, st->status, status, n, &d_status));
+  if (is_f64(c))
+    CHK(launch_prep_query<Field64Ops>(c, st, n, d_status));
+  else
+    CHK(launch_prep_query<Field128Ops>(c, st, n, d_status));
+  CHK(copy_out(c, out_prep_shares, st->prep.p, n * c->cfg.prep_share_len));
+  CHK(copy_out(c, status, d_status, n));
+  return finish_call(c, {out_prep_shares, status});
+}
+
+int prio3gpu_ctx_set_async(prio3gpu_ctx* c, int on) {
+  if (!c) return PRIO3GPU_E_ARG;
+  c->async_mode = on != 0;
   return 0;
+}
+
+int prio3gpu_ctx_mark(prio3gpu_ctx* c, int* out_mark) {
+  if (!c || !out_mark) {
+    set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const int k = c->ev_next;
+  c->ev_next = (c->ev_next + 1) % prio3gpu_ctx::kMarks;
+  if (!c->ev[k]) HIPCHK(hipEventCreateWithFlags(&c->ev[k], hipEventDisableTiming));
+  HIPCHK(hipEventRecord(c->ev[k], c->stream));
+  *out_mark = k;
+  return 0;
+}
+
+int prio3gpu_ctx_wait_mark(prio3gpu_ctx* c, prio3gpu_ctx* other, int mark) {
+  if (!c || !other || mark < 0 || mark >= prio3gpu_ctx::kMarks || !other->ev[mark]) {
+    set_err("bad mark");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamWaitEvent(c->stream, other->ev[mark], 0));
+  return 0;
+}
+
+int prio3gpu_ctx_wait(prio3gpu_ctx* c, prio3gpu_ctx* other) {
+  if (!c || !other) {
+    set_err("null context");
+    return PRIO3GPU_E_ARG;
+  }
+  if (c == other) return 0;
+  int m = 0;
+  CHK(prio3gpu_ctx_mark(other, &m));
+  return prio3gpu_ctx_wait_mark(c, other, m);
 }
 
 int prio3gpu_prepare_shares_to_prepare_message(prio3gpu_ctx* c, size_t n,
@@ -1337,8 +1501,7 @@ int prio3gpu_prepare_shares_to_prepare_message(prio3gpu_ctx* c, size_t n,
     CHK(launch_decide<Field128Ops>(c, n, d_l, d_h, d_msg, d_status));
   CHK(copy_out(c, out_prep_msgs, d_msg, n * g.prep_msg_len));
   CHK(copy_out(c, status, d_status, n));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  return finish_call(c, {leader_prep_shares, helper_prep_shares, out_prep_msgs, status});
 }
 
 int prio3gpu_prepare_next(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* prep_msgs,
@@ -1394,8 +1557,7 @@ int prio3gpu_prepare_next(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const u
       CHK(launch_accumulate<Field128Ops>(c, st, n, batch_slots, d_status, agg));
   }
   CHK(copy_out(c, status, d_status, n));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  return finish_call(c, {prep_msgs, status, out_output_shares, batch_slots});
 }
 
 int prio3gpu_helper_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* nonces,
@@ -1447,8 +1609,8 @@ int prio3gpu_helper_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const ui
   }
   CHK(copy_out(c, out_prep_msgs, d_msg, n * g.prep_msg_len));
   CHK(copy_out(c, status, d_status, n));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  return finish_call(c, {nonces, public_shares, helper_input_shares, leader_prep_shares,
+                         batch_slots, out_prep_msgs, status});
 }
 
 int prio3gpu_random_size(const prio3gpu_ctx* c) {

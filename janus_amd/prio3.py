@@ -273,6 +273,39 @@ class Prio3Gpu:
     def sync(self):
         check(lib().prio3gpu_ctx_sync(self._ctx), "sync")
 
+    # -- asynchronous use (include/prio3gpu.h: prio3gpu_ctx_set_async / _wait / _mark) -----------
+    def set_async(self, on: bool = True):
+        """Calls over device buffers return once queued (host buffers still wait)."""
+        check(lib().prio3gpu_ctx_set_async(self._ctx, int(bool(on))), "ctx_set_async")
+
+    def wait_for(self, other: "Prio3Gpu", mark: Optional[int] = None):
+        """Work queued here from now on starts after `other`'s work queued so far (or up to
+        `mark`, from other.mark())."""
+        if mark is None:
+            check(lib().prio3gpu_ctx_wait(self._ctx, other._ctx), "ctx_wait")
+        else:
+            check(lib().prio3gpu_ctx_wait_mark(self._ctx, other._ctx, mark), "ctx_wait_mark")
+
+    def mark(self) -> int:
+        m = ctypes.c_int()
+        check(lib().prio3gpu_ctx_mark(self._ctx, ctypes.byref(m)), "ctx_mark")
+        return m.value
+
+    def prepare_init_xof(self, state: PrepareState, nonces, public_shares, input_shares, status):
+        """prepare_init's XOF phase (query + joint randomness, helper expansion); `status` (n,)
+        uint8, host or device; inputs must stay valid until prepare_init_query."""
+        n = _nbytes(status)
+        check(lib().prio3gpu_prepare_init_xof(self._ctx, state._h, n, _ptr(nonces),
+                                              _ptr(public_shares), _ptr(input_shares),
+                                              _ptr(status)), "prepare_init_xof")
+        state._keep = input_shares
+
+    def prepare_init_query(self, state: PrepareState, out_prep_shares, status):
+        """prepare_init's FLP-query phase -> prep shares into `out_prep_shares` (n, prep_share)."""
+        n = _nbytes(status)
+        check(lib().prio3gpu_prepare_init_query(self._ctx, state._h, n, _ptr(out_prep_shares),
+                                                _ptr(status)), "prepare_init_query")
+
     def new_state(self, agg_id: int, capacity: int) -> PrepareState:
         return PrepareState(self, agg_id, capacity)
 
