@@ -1,0 +1,89 @@
+"""Asynchronous engine use (include/prio3gpu.h: prio3gpu_ctx_set_async / _mark / _wait_mark and
+prepare_init split into its XOF and FLP-query phases): a leader context and a helper context
+queue two batches with cross-context marks only (no host waits between calls), and the results
+equal the synchronous path's / the oracle's."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "sum8"])
+def test_async_two_context_pipeline_matches_oracle(name):
+    import torch
+    from janus_amd._lib import check, lib
+    from janus_amd.prio3 import Prio3Gpu
+    from tests.reports import CONFIGS, expected_aggregate, make_batch
+    b = make_batch(name, 40)
+    c = CONFIGS[name]
+    mk = lambda: Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"], length=c["length"],
+                          chunk_length=c["chunk"])
+    A, H = mk(), mk()
+    s = A.sizes
+    dev = torch.device("cuda", 0)
+    halves = [slice(0, 20), slice(20, 40)]
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    nz, pub, lin, hin = d(b.nonces), d(b.public), d(b.leader_in), d(b.helper_in)
+    times = torch.arange(b.n, dtype=torch.int64, device=dev) + 5000
+    lprep = torch.zeros((b.n, s.prep_share), dtype=torch.uint8, device=dev)
+    hprep = torch.zeros((b.n, s.prep_share), dtype=torch.uint8, device=dev)
+    msgs = torch.zeros((b.n, max(1, s.prep_msg)), dtype=torch.uint8, device=dev)
+    lst = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    hst = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    A.set_async(True)
+    H.set_async(True)
+    P = lambda t: t.data_ptr()
+    ls = [A.new_state(0, 20), A.new_state(0, 20)]
+    hs = H.new_state(1, 20)
+    lagg, hagg = A.new_aggregate(1), H.new_aggregate(1)
+    for i, j in enumerate(halves):
+        A.prepare_init_xof(ls[i], nz[j], pub[j] if s.public_share else None, lin[j], lst[j])
+        A.prepare_init_query(ls[i], lprep[j], lst[j])
+        mA = A.mark()
+        H.prepare_init_xof(hs, nz[j], pub[j] if s.public_share else None, hin[j], hst[j])
+        H.prepare_init_query(hs, hprep[j], hst[j])
+        H.wait_for(A, mA)
+        check(lib().prio3gpu_prepare_shares_to_prepare_message(
+            H._ctx, 20, P(lprep[j]), P(hprep[j]), P(msgs[j]) if s.prep_msg else None,
+            P(hst[j])), "decide")
+        check(lib().prio3gpu_prepare_next(H._ctx, hs._h, 20, P(msgs[j]) if s.prep_msg else None,
+                                          P(hst[j]), None, None, hagg._h), "helper next")
+        check(lib().prio3gpu_agg_update_reports(hagg._h, 20, P(nz[j]), P(times[j]), P(hst[j]),
+                                                None), "helper meta")
+        mH = H.mark()
+        A.wait_for(H, mH)
+        check(lib().prio3gpu_prepare_next(A._ctx, ls[i]._h, 20, P(msgs[j]) if s.prep_msg else None,
+                                          P(lst[j]), None, None, lagg._h), "leader next")
+    A.sync()
+    H.sync()
+    A.set_async(False)
+    H.set_async(False)
+    assert int(lst.max()) == 0 and int(hst.max()) == 0
+    np.testing.assert_array_equal(lprep.cpu().numpy(), b.leader_prep)
+    np.testing.assert_array_equal(hprep.cpu().numpy(), b.helper_prep)
+    if s.prep_msg:
+        np.testing.assert_array_equal(msgs.cpu().numpy(), b.prep_msg)
+    for agg, which in ((lagg, "leader"), (hagg, "helper")):
+        got, cnt = agg.read(0)
+        want, wcnt = expected_aggregate(b, which)
+        assert got == want and cnt == wcnt == b.n
+    ck, (start, dur) = hagg.read_reports(0)
+    assert start == 5000 and dur == b.n
+
+
+@pytest.mark.gpu
+def test_query_phase_without_xof_phase_is_an_error():
+    from janus_amd.prio3 import Prio3Gpu, Prio3GpuError
+    from tests.reports import CONFIGS, make_batch
+    b = make_batch("sum8", 4)
+    c = CONFIGS["sum8"]
+    v = Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"])
+    st = v.new_state(0, 4)
+    status = np.zeros(4, np.uint8)
+    with pytest.raises(Prio3GpuError):
+        v.prepare_init_query(st, np.zeros((4, v.sizes.prep_share), np.uint8), status)
+    v.prepare_init_xof(st, b.nonces, b.public, b.leader_in, status)
+    out = np.zeros((4, v.sizes.prep_share), np.uint8)
+    v.prepare_init_query(st, out, status)
+    assert (status == 0).all() and (out == b.leader_prep).all()

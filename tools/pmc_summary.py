@@ -22,28 +22,52 @@ def short(name):
 
 
 def load_counters(d):
+    """Per-kernel counter values averaged over the FULL-SIZE dispatches (those with the kernel's
+    largest grid: the bench's timed batches, not its small parity-gate batch)."""
     if not d:
         return {}
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-    agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    disp = collections.defaultdict(set)
+    rows = collections.defaultdict(lambda: collections.defaultdict(dict))  # k -> disp -> {..}
+    grid = {}
     for f in files:
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
-            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[k].add(r["Dispatch_Id"])
-    return {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in agg.items()}
+            dsp = r["Dispatch_Id"]
+            rows[k][dsp][r["Counter_Name"]] = rows[k][dsp].get(r["Counter_Name"], 0.0) + \
+                float(r["Counter_Value"])
+            grid[(k, dsp)] = int(r["Grid_Size"])
+    out = {}
+    for k, disp in rows.items():
+        gmax = max(grid[(k, dsp)] for dsp in disp)
+        full = [c for dsp, c in disp.items() if grid[(k, dsp)] == gmax]
+        names = set().union(*full)
+        out[k] = {c: sum(x.get(c, 0.0) for x in full) / len(full) for c in names}
+        out[k]["dispatches_full"] = len(full)
+    return out
 
 
 def load_trace(d):
-    files = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    """Per-kernel durations: all dispatches (kernel_stats.csv) and the full-size ones (largest
+    grid, from kernel_trace.csv) -- `avg_ms` is the full-size average, the number the bench's HIP
+    events time."""
     out = {}
-    for f in files:
+    for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            out[short(r["Name"])] = {"calls": int(r["Calls"]),
-                                      "avg_ms": float(r["AverageNs"]) / 1e6,
+            out[short(r["Name"])] = {"calls_all": int(r["Calls"]),
+                                      "avg_ms_all": float(r["AverageNs"]) / 1e6,
                                       "total_ms": float(r["TotalDurationNs"]) / 1e6,
                                       "pct": float(r["Percentage"])}
+    disp = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+            disp[short(r["Kernel_Name"])].append(
+                (g, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+    for k, v in disp.items():
+        gmax = max(g for g, _ in v)
+        full = [t for g, t in v if g == gmax]
+        e = out.setdefault(k, {})
+        e.update({"calls": len(full), "avg_ms": sum(full) / len(full), "grid": gmax})
     return out
 
 
