@@ -222,8 +222,10 @@ int prio3gpu_helper_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const 
 
 /* Client::shard for n reports (prio 0.15.1 shard_with_random; SURVEY §8(f) #1: batched client
  * shard + FLP prove, used to generate inputs at scale).
- *   measurements  n x (SUMVEC ? length : 1) u64 (Count 0/1, Sum value, SumVec entries, Histogram
- *                 bucket index)
+ *   measurements  n x (SUMVEC or FPVEC ? length : 1) u64 (Count 0/1, Sum value, SumVec entries,
+ *                 Histogram bucket index, FixedPoint raw two's-complement entries whose L2 norm
+ *                 is < 1 -- prio's shard rejects others; here they yield reports that fail
+ *                 verification; client/src/lib.rs:212-258)
  *   rand          n x prio3gpu_random_size() bytes, prio order:
  *                 k_meas, k_proof, [blind_helper, blind_leader], k_prove
  *   outputs       public shares, leader input shares, helper input shares (DAP encodings)

@@ -1646,10 +1646,17 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
     hipLaunchKernelGGL(k_expand<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, 1u,
                        CRows{d_helper, g.helper_share_len}, hm, hp, (const uint8_t*)nullptr);
   }
+  uint64_t* d_norms = nullptr;  // FixedPointBoundedL2VecSum: squared norm per measurement
+  if (g.kind == KIND_FPVEC) {
+    CHK(c->io[5].ensure(n * 16));
+    d_norms = reinterpret_cast<uint64_t*>(c->io[5].p);
+    PROF(KID_SHARD_MEAS);
+    hipLaunchKernelGGL(k_shard_norm, dim3(N), dim3(256), 0, c->stream, g, N, d_meas, d_norms);
+  }
   {
     PROF(KID_SHARD_MEAS);
     hipLaunchKernelGGL(k_shard_meas<FO>, dim3((g.meas_len + 255) / 256, N), dim3(256), 0,
-                       c->stream, g, N, d_meas, mw, CRows{hm.base, hm.stride}, leader);
+                       c->stream, g, N, d_meas, mw, CRows{hm.base, hm.stride}, leader, d_norms);
   }
   {
     PROF(KID_SHARD_JR);
@@ -1660,8 +1667,9 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
   }
   {
     PROF(KID_PROVE);
-    const uint32_t cc = (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM) ? g.chunk : 1u;
-    const size_t lds = sizeof(typename FO::T) * (8 * (size_t)g.m + cc + 1 + g.calls + 1) + 16;
+    const uint32_t cc =
+        (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM || g.kind == KIND_FPVEC) ? g.chunk : 1u;
+    const size_t lds = sizeof(typename FO::T) * (6 * (size_t)g.m + cc + 1 + g.calls + 1) + 16;
     if (lds > 160 * 1024) {
       set_err("prove LDS requirement %zu too large", lds);
       return PRIO3GPU_E_ARG;
@@ -1669,7 +1677,7 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
     hipLaunchKernelGGL(k_flp_prove<FO>, dim3(N), dim3(256), lds, c->stream, g, N,
                        c->twiddles2.u8(), d_meas, mw,
                        CRows{d_prand, (size_t)std::max<uint32_t>(g.prove_rand_len, 1) * es},
-                       CRows{d_jr, 32}, Rows{d_proof, (size_t)g.proof_len * es});
+                       CRows{d_jr, 32}, Rows{d_proof, (size_t)g.proof_len * es}, d_norms);
   }
   {
     PROF(KID_SHARD_PROOF);
@@ -1698,13 +1706,9 @@ int prio3gpu_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t*
     set_err("null argument");
     return PRIO3GPU_E_ARG;
   }
-  if (c->cfg.kind == KIND_FPVEC) {
-    set_err("shard: FixedPointBoundedL2VecSum clients are not batched on the GPU");
-    return PRIO3GPU_E_ARG;
-  }
   HIPCHK(hipSetDevice(c->device));
   const Cfg& g = c->cfg;
-  const uint32_t mw = g.kind == KIND_SUMVEC ? g.length : 1u;
+  const uint32_t mw = (g.kind == KIND_SUMVEC || g.kind == KIND_FPVEC) ? g.length : 1u;
   const size_t rs = (size_t)prio3gpu_random_size(c);
   const uint8_t *d_nonces, *d_meas, *d_rand;
   CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));

@@ -1861,12 +1861,60 @@ namespace p3g {
 
 // Encoded measurement element i (0/1 for every type here) from the raw measurement row
 // (SumVec: `length` u64 entries, others: one u64).  prio Type::encode_measurement.
-DEVI uint32_t enc_meas_bit(const Cfg& cfg, const uint64_t* m, uint32_t i) {
+// Bit i of the encoded measurement.  FixedPointBoundedL2VecSum (prio fixedpoint_l2.rs encode):
+// entry e contributes the n bits of z_e = v_e + 2^(n-1) (v_e the raw two's-complement fixed-point
+// value), then the 2n-2 bits of the squared norm sum_e v_e^2 (`norm`: two LE u64 words).
+DEVI uint32_t enc_meas_bit(const Cfg& cfg, const uint64_t* m, uint32_t i,
+                           const uint64_t* norm = nullptr) {
   switch (cfg.kind) {
     case KIND_COUNT: return (uint32_t)(m[0] & 1u);
     case KIND_SUM: return (uint32_t)((m[0] >> i) & 1u);
     case KIND_SUMVEC: return (uint32_t)((m[i / cfg.bits] >> (i % cfg.bits)) & 1u);
+    case KIND_FPVEC: {
+      const uint32_t nb = cfg.bits, ent = i / nb;
+      if (ent < cfg.length) {
+        const uint64_t z = m[ent] + (1ull << (nb - 1));
+        return (uint32_t)((z >> (i - ent * nb)) & 1u);
+      }
+      const uint32_t b = i - cfg.length * nb;  // norm bit
+      return (uint32_t)((norm[b >> 6] >> (b & 63u)) & 1u);
+    }
     default: return m[0] == i ? 1u : 0u;  // Histogram one-hot
+  }
+}
+
+// FixedPointBoundedL2VecSum client: squared L2 norm sum_e v_e^2 of each measurement (u128, two LE
+// words; the caller's entries satisfy the norm bound < 2^(2n-2), which prio's shard checks).
+// Block per report.
+__global__ void __launch_bounds__(256) k_shard_norm(Cfg cfg, uint32_t n, const uint64_t* meas,
+                                                    uint64_t* norms) {
+  typedef unsigned __int128 u128;
+  __shared__ uint64_t red[2 * 256];
+  const uint32_t r = blockIdx.x;
+  if (r >= n) return;
+  const int64_t* mr = reinterpret_cast<const int64_t*>(meas) + (size_t)r * cfg.length;
+  u128 acc = 0;
+  for (uint32_t e = threadIdx.x; e < cfg.length; e += blockDim.x) {
+    const int64_t v = mr[e];
+    const uint64_t a = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    acc += (u128)a * a;
+  }
+  red[2 * threadIdx.x] = (uint64_t)acc;
+  red[2 * threadIdx.x + 1] = (uint64_t)(acc >> 64);
+  __syncthreads();
+  for (uint32_t sft = blockDim.x / 2; sft > 0; sft >>= 1) {
+    if (threadIdx.x < sft) {
+      const u128 a = ((u128)red[2 * threadIdx.x + 1] << 64) | red[2 * threadIdx.x];
+      const u128 b = ((u128)red[2 * (threadIdx.x + sft) + 1] << 64) | red[2 * (threadIdx.x + sft)];
+      const u128 c = a + b;
+      red[2 * threadIdx.x] = (uint64_t)c;
+      red[2 * threadIdx.x + 1] = (uint64_t)(c >> 64);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    norms[2 * r] = red[0];
+    norms[2 * r + 1] = red[1];
   }
 }
 
@@ -1900,33 +1948,40 @@ DEVI void ntt_lds(typename FO::T* A, typename FO::T* B, uint32_t n, uint32_t log
 // G of the wire polys' values there (iNTT -> twist by w^d / m -> NTT).  Interpolating those 2m
 // values gives the 2m-1 proof coefficients.
 // tw2 = [w^0 .. w^(2m-1), 1/m, 1/(2m)] (w = primitive 2m-th root), Montgomery.
-// LDS: FA[m] FB[m] GA[m] GB[m] PE[m] PO[m] G[2m] RP[c+1] RR[calls+1]
+// LDS: FA[m] FB[m] GA[m] GB[m] PE[m] PO[m] RP[c+1] RR[calls+1]; G[2m] reuses FA..GB at the end.
+// FixedPointBoundedL2VecSum: gadget 0 is the ParallelSum(Mul) range check above (chunk c0 over
+// the entry and norm bits); gadget 1, ParallelSum(PolyEval(x^2 - 2^n x + 2^(2n-2)), c1) =
+// sum_j (w_j - 2^(n-1))^2 over the decoded entries z_e (padding 2^(n-1) = the encoded zero, with
+// num_shares = 1), follows in the same block with m1 | m, its roots taken from tw2 at stride m/m1.
 template <class FO>
 __global__ void __launch_bounds__(256) k_flp_prove(Cfg cfg, uint32_t n, const uint8_t* tw2,
                                                    const uint64_t* meas, uint32_t meas_words,
-                                                   CRows prove_rand, CRows jr, Rows proof_out) {
+                                                   CRows prove_rand, CRows jr, Rows proof_out,
+                                                   const uint64_t* norms) {
   using T = typename FO::T;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t r = blockIdx.x;
   if (r >= n) return;
   const uint32_t tid = threadIdx.x, nthr = blockDim.x;
   const uint32_t m = cfg.m, logm = cfg.logm, calls = cfg.calls;
-  const uint32_t c = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) ? cfg.chunk : 1u;
+  const bool psum =
+      (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM || cfg.kind == KIND_FPVEC);
+  const uint32_t c = psum ? cfg.chunk : 1u;
   T* FA = reinterpret_cast<T*>(smem);
   T* FB = FA + m;
   T* GA = FB + m;
   T* GB = GA + m;
   T* PE = GB + m;
   T* PO = PE + m;
-  T* G = PO + m;
-  T* RP = G + 2 * m;
+  T* G = FA;  // after the wire loop
+  T* RP = PO + m;
   T* RR = RP + (c + 1);
   const uint64_t* mrow = meas + (size_t)r * meas_words;
+  const uint64_t* nrm = norms ? norms + 2 * (size_t)r : nullptr;
   const uint8_t* pr = prove_rand.at(r);
   const T one = FO::one_mont();
   const T inv_m = FO::load(tw2 + (size_t)(2 * m) * FO::ES);
   const T inv_2m = FO::load(tw2 + (size_t)(2 * m + 1) * FO::ES);
-  const bool psum = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM);
   // r powers for the a-wires (ParallelSum types): RP[i] = r^i (i <= c), RR[q] = (r^c)^q
   {
     const uint32_t wave = tid >> 6, lane = tid & 63;
@@ -1959,7 +2014,7 @@ __global__ void __launch_bounds__(256) k_flp_prove(Cfg cfg, uint32_t n, const ui
         if (psum) {
           const uint32_t idx = (k - 1) * c + j;
           if (idx < cfg.meas_len) {
-            const uint32_t x = enc_meas_bit(cfg, mrow, idx);
+            const uint32_t x = enc_meas_bit(cfg, mrow, idx, nrm);
             a = x ? FO::mul(RP[j + 1], RR[k - 1]) : FO::zero();  // r^(idx+1) x
             b = x ? FO::zero() : FO::neg(one);                  // x - 1
           } else {
@@ -2011,6 +2066,65 @@ __global__ void __launch_bounds__(256) k_flp_prove(Cfg cfg, uint32_t n, const ui
   }
   for (uint32_t w = tid; w < arity; w += nthr)
     FO::store(out + (size_t)w * FO::ES, FO::load(pr + (size_t)w * FO::ES));
+  if constexpr (FO::ES == 16) {
+  if (cfg.kind != KIND_FPVEC) return;
+
+  // ---- gadget 1 (FixedPointBoundedL2VecSum): sum_j (w_j - 2^(n-1))^2, m1 | m ----
+  __syncthreads();
+  const uint32_t m1 = cfg.m1, logm1 = cfg.logm1, calls1 = cfg.calls1, c1 = cfg.chunk1;
+  const uint32_t q = m / m1;  // tw2 stride for the 2*m1-th roots is q, for the m1-th roots 2q
+  const T qm = FO::to_mont(FO::from_u32(q));
+  const T inv_m1 = FO::mul(inv_m, qm), inv_2m1 = FO::mul(inv_2m, qm);
+  const uint32_t nb = cfg.bits;
+  const T half_one = FO::to_mont(FO::from_u64x2(1ull << (nb - 1), 0ull));  // 2^(n-1)
+  for (uint32_t k = tid; k < m1; k += nthr) {
+    PE[k] = FO::zero();
+    PO[k] = FO::zero();
+  }
+  __syncthreads();
+  const uint8_t* pr1 = pr + (size_t)arity * FO::ES;  // gadget-1 wire seeds
+  for (uint32_t j = 0; j < c1; ++j) {
+    for (uint32_t k = tid; k < m1; k += nthr) {
+      T a = FO::zero();
+      if (k == 0) {
+        a = FO::to_mont(FO::load(pr1 + (size_t)j * FO::ES));
+      } else if (k <= calls1) {
+        const uint32_t e = (k - 1) * c1 + j;
+        a = e < cfg.length ? FO::to_mont(FO::from_u64x2(mrow[e] + (1ull << (nb - 1)), 0ull))
+                           : half_one;
+      }
+      const T d = FO::sub(a, half_one);
+      PE[k] = FO::add(PE[k], FO::mul(d, d));
+      FA[bitrev(k, logm1)] = a;
+    }
+    __syncthreads();
+    ntt_lds<FO>(FA, nullptr, m1, logm1, tw2, 2 * q, tid, nthr);
+    for (uint32_t d = tid; d < m1; d += nthr) {
+      const uint32_t src = (m1 - d) & (m1 - 1);
+      const T s = FO::mul(FO::load(tw2 + (size_t)(d * q) * FO::ES), inv_m1);
+      GA[bitrev(d, logm1)] = FO::mul(FA[src], s);
+    }
+    __syncthreads();
+    ntt_lds<FO>(GA, nullptr, m1, logm1, tw2, 2 * q, tid, nthr);
+    for (uint32_t k = tid; k < m1; k += nthr) {
+      const T dd = FO::sub(GA[k], half_one);
+      PO[k] = FO::add(PO[k], FO::mul(dd, dd));
+    }
+    __syncthreads();
+  }
+  const uint32_t m12 = 2 * m1, logm12 = logm1 + 1;
+  for (uint32_t i = tid; i < m12; i += nthr)
+    G[bitrev(i, logm12)] = (i & 1) ? PO[i >> 1] : PE[i >> 1];
+  __syncthreads();
+  ntt_lds<FO>(G, nullptr, m12, logm12, tw2, q, tid, nthr);
+  uint8_t* out1 = out + (size_t)(arity + cfg.gp_len) * FO::ES;
+  for (uint32_t d = tid; d < cfg.gp_len1; d += nthr) {
+    const T v = FO::mul(G[(m12 - d) & (m12 - 1)], inv_2m1);
+    FO::store(out1 + (size_t)(c1 + d) * FO::ES, FO::from_mont(v));
+  }
+  for (uint32_t w = tid; w < c1; w += nthr)
+    FO::store(out1 + (size_t)w * FO::ES, FO::load(pr1 + (size_t)w * FO::ES));
+  }
 }
 
 // Shard helpers (lane per report).  rand row = [k_meas, k_proof, (blind_h, blind_l,) k_prove].
@@ -2035,11 +2149,12 @@ __global__ void __launch_bounds__(256) k_shard_seeds(Cfg cfg, uint32_t n, CRows 
 template <class FO>
 __global__ void __launch_bounds__(256) k_shard_meas(Cfg cfg, uint32_t n, const uint64_t* meas,
                                                     uint32_t meas_words, CRows helper_meas,
-                                                    Rows leader) {
+                                                    Rows leader, const uint64_t* norms) {
   const uint32_t r = blockIdx.y;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n || i >= cfg.meas_len) return;
-  const uint32_t x = enc_meas_bit(cfg, meas + (size_t)r * meas_words, i);
+  const uint32_t x = enc_meas_bit(cfg, meas + (size_t)r * meas_words, i,
+                                  norms ? norms + 2 * (size_t)r : nullptr);
   const typename FO::T h = FO::load(helper_meas.at(r) + (size_t)i * FO::ES);
   FO::store(leader.at(r) + (size_t)i * FO::ES, FO::sub(FO::from_u32(x), h));
 }

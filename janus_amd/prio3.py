@@ -397,12 +397,16 @@ class Prio3Gpu:
 
     def shard(self, state: PrepareState, nonces, measurements, rand, out=None):
         """Batched `Client::shard` (prio shard_with_random) on the GPU -> (public shares, leader
-        input shares, helper input shares).  `measurements`: (n,) or (n, length) uint64."""
+        input shares, helper input shares).  `measurements`: (n,) or (n, length) uint64; for
+        FixedPointBoundedL2VecSum the (n, length) raw two's-complement fixed-point integers
+        (int64 accepted), whose L2 norm must be < 1 as prio's shard requires."""
         s = self.sizes
         n = _nbytes(nonces) // 16
         nonces = _as_u8(nonces, n, 16, "nonces")
         rand = _as_u8(rand, n, self.random_size(), "rand")
         if isinstance(measurements, np.ndarray):
+            if measurements.dtype == np.int64:
+                measurements = np.ascontiguousarray(measurements).view(np.uint64)
             measurements = np.ascontiguousarray(measurements, dtype=np.uint64)
         if out is None:
             out = (np.zeros((n, s.public_share), np.uint8) if s.public_share else None,

@@ -103,7 +103,11 @@ def make_batch(name: str, n: int, cfg_id: bytes = None, start: int = 0, xof=None
 
 
 def meas_array(b: Batch) -> np.ndarray:
-    """Measurements as the (n, words) uint64 array prio3gpu_shard takes."""
+    """Measurements as the (n, words) array prio3gpu_shard takes (uint64; FixedPoint vectors:
+    int64 raw two's-complement entries)."""
+    from oracle.prio3 import FixedPointBoundedL2VecSum
+    if isinstance(b.vdaf.typ, FixedPointBoundedL2VecSum):
+        return np.array(b.measurements, dtype=np.int64)
     if isinstance(b.measurements[0], list):
         return np.array(b.measurements, dtype=np.uint64)
     return np.array(b.measurements, dtype=np.uint64).reshape(-1, 1)

@@ -8,9 +8,13 @@ prepare_init run concurrently on two engine contexts (two HIP streams): they are
 decide, like Janus's leader and helper processes.  Inputs: U distinct reports from the C
 restatement (SURVEY §8(d) recipe, oracle/prio3_ref.c), tiled to B on the GPU -- every tile is
 processed in full; the aggregate is checked against the C restatement's aggregate x tiles.
-CPU baseline: the C restatement on the same reports, 16 threads.
+With --distinct 1 the B reports are all distinct: the SURVEY §8(d) recipe's nonces, randomness
+and measurements (C restatement) go through the GPU client shard (prio3gpu_shard, Client::shard
++ FLP prove; the first U are checked byte for byte against the C restatement's shard) and the
+check is unshard(leader + helper aggregate) == the plaintext fixed-point sum.
+CPU baseline: the C restatement on U reports, 16 threads.
 
-python tools/bench_fpvec.py [--reports B --unique U --steps K --entries E --bits N]
+python tools/bench_fpvec.py [--reports B --unique U --steps K --entries E --bits N --distinct 1]
 """
 import argparse
 import ctypes
@@ -36,6 +40,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--overlap", type=int, default=1)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--distinct", type=int, default=0)
+    ap.add_argument("--shard-chunk", type=int, default=2048)
     args = ap.parse_args()
 
     import torch
@@ -45,7 +51,7 @@ def main():
     from oracle.ref import Prio3Ref
 
     B, U = args.reports, min(args.unique, args.reports)
-    assert B % U == 0
+    assert args.distinct or B % U == 0
     cid = b"cfgE-%d-%d" % (args.bits, args.entries)
     vk = O.synth_verify_key(cid)
     ref = Prio3Ref(4, vk, args.bits, args.entries, 0)
@@ -62,16 +68,51 @@ def main():
           f"({cpu_rate:.1f} reports/s, {args.threads} threads)", flush=True)
 
     dev = torch.device("cuda:0")
-    tiles = B // U
-
-    def tile(a):
-        return torch.from_numpy(np.ascontiguousarray(a)).to(dev).repeat(tiles, 1).contiguous()
-
-    d_nonces, d_pub, d_lin, d_hin = (tile(g[k]) for k in ("nonces", "public", "leader_in",
-                                                          "helper_in"))
+    tiles = B // U if not args.distinct else 1
     vl = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(args.bits, args.entries, vk)
     vh = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(args.bits, args.entries, vk)
     s = vl.sizes
+    shard_info = None
+    if args.distinct:
+        # B distinct reports: recipe inputs from the C restatement, shares from the GPU shard
+        d_nonces = torch.empty((B, 16), dtype=torch.uint8, device=dev)
+        d_pub = torch.empty((B, s.public_share), dtype=torch.uint8, device=dev)
+        d_lin = torch.empty((B, s.leader_input_share), dtype=torch.uint8, device=dev)
+        d_hin = torch.empty((B, s.helper_input_share), dtype=torch.uint8, device=dev)
+        plain = np.zeros(args.entries, np.int64)
+        CH = min(args.shard_chunk, B)
+        sst = vh.new_state(1, CH)
+        t_syn = t_sh = 0.0
+        for i in range(0, B, CH):
+            k = min(CH, B - i)
+            t0 = time.time()
+            syn = ref.synth(cid, i, k, threads=args.threads)
+            t_syn += time.time() - t0
+            plain += syn["meas"].view(np.int64).sum(axis=0)
+            d_nonces[i:i + k] = torch.from_numpy(syn["nonces"]).to(dev)
+            t0 = time.time()
+            vh.shard(sst, d_nonces[i:i + k], torch.from_numpy(syn["meas"].view(np.int64)).to(dev),
+                     torch.from_numpy(syn["rand"]).to(dev),
+                     out=(d_pub[i:i + k], d_lin[i:i + k], d_hin[i:i + k]))
+            torch.cuda.synchronize()
+            t_sh += time.time() - t0
+        sst.close()
+        del sst
+        k = min(U, B)
+        assert np.array_equal(d_lin[:k].cpu().numpy(), g["leader_in"][:k]), "GPU shard != C"
+        assert np.array_equal(d_hin[:k].cpu().numpy(), g["helper_in"][:k]), "GPU shard != C"
+        assert np.array_equal(d_pub[:k].cpu().numpy(), g["public"][:k]), "GPU shard != C"
+        shard_info = {"reports": B, "synth_s": round(t_syn, 2), "gpu_shard_s": round(t_sh, 2),
+                      "gpu_shard_reports_per_s": round(B / t_sh, 1),
+                      "cpu_gen_reports_per_s": round(U / t_gen, 2),
+                      "check": f"first {k} GPU shares == C restatement bytes"}
+        print("# " + json.dumps(shard_info), flush=True)
+    else:
+        def tile(a):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(dev).repeat(tiles, 1).contiguous()
+
+        d_nonces, d_pub, d_lin, d_hin = (tile(g[k]) for k in ("nonces", "public", "leader_in",
+                                                              "helper_in"))
     ls, hs = vl.new_state(0, B), vh.new_state(1, B)
     lagg, hagg = vl.new_aggregate(1), vh.new_aggregate(1)
     d_lprep = torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
@@ -143,11 +184,18 @@ def main():
     assert lc == hc == B * args.steps
     mult = tiles * args.steps
     p = O.Field128.MODULUS
-    for got, exp in ((la, res["agg_l"]), (ha, res["agg_h"])):
-        e = O.Field128.decode_vec(exp.tobytes())
-        assert O.Field128.decode_vec(got) == [(x * mult) % p for x in e], "aggregate mismatch"
+    if args.distinct:
+        # unshard(leader + helper) == plaintext sum of the fixed-point values (x steps)
+        got = vl.unshard([la, ha], num_measurements=B * args.steps)
+        want = [float(x) * args.steps * 2.0 ** (1 - args.bits) for x in plain]
+        assert got == want, "aggregate != plaintext sum"
+    else:
+        for got, exp in ((la, res["agg_l"]), (ha, res["agg_h"])):
+            e = O.Field128.decode_vec(exp.tobytes())
+            assert O.Field128.decode_vec(got) == [(x * mult) % p for x in e], "aggregate mismatch"
     out = {"config": f"Prio3FixedPoint{args.bits}BitBoundedL2VecSum entries={args.entries}",
-           "reports_per_step": B, "unique": U, "ms_per_step": dt * 1e3,
+           "reports_per_step": B, "unique": B if args.distinct else U,
+           "gpu_shard": shard_info, "ms_per_step": dt * 1e3,
            "reports_per_sec": B / dt, "overlap_leader_helper": bool(args.overlap),
            "cpu_baseline": {"reports_per_sec": cpu_rate, "threads": args.threads,
                             "kind": "port", "sample": f"{U} reports"},
