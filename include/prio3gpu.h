@@ -269,7 +269,7 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg*
                            prio3gpu_agg* total);
 
 /* Per-kernel timing with HIP events on the context's stream (opt-in; bench.py uses it for the
- * live roofline numbers).  prof_read returns the number of kernel ids and fills, per kernel id,
+ * live roofline numbers).  prof_read returns min(kernel ids, max_kernels) and fills, per kernel id,
  * the summed milliseconds and launch count since the last read. */
 int prio3gpu_prof_enable(prio3gpu_ctx* ctx, int on);
 int prio3gpu_prof_read(prio3gpu_ctx* ctx, double* ms, uint64_t* launches, int max_kernels);

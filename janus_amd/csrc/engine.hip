@@ -140,7 +140,7 @@ enum KernelId {
   KID_FLP_WIRES, KID_FPV_WEIGHTS, KID_FPV_WIRES0, KID_FPV_WIRES1, KID_FPV_FINAL, KID_DECIDE,
   KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
   KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
-  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE,
+  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM,
   KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
@@ -148,7 +148,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_flp_wires", "k_fpv_weights", "k_fpv_wires0", "k_fpv_wires1", "k_fpv_finalize", "k_decide",
     "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
     "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
-    "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave"};
+    "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave", "k_shard_norm"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -1650,7 +1650,7 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
   if (g.kind == KIND_FPVEC) {
     CHK(c->io[5].ensure(n * 16));
     d_norms = reinterpret_cast<uint64_t*>(c->io[5].p);
-    PROF(KID_SHARD_MEAS);
+    PROF(KID_SHARD_NORM);
     hipLaunchKernelGGL(k_shard_norm, dim3(N), dim3(256), 0, c->stream, g, N, d_meas, d_norms);
   }
   {
@@ -1964,7 +1964,7 @@ int prio3gpu_prof_read(prio3gpu_ctx* c, double* ms, uint64_t* launches, int max_
     c->prof.pool.push_back(r.b);
   }
   c->prof.recs.clear();
-  return KID_COUNT;
+  return std::min<int>(KID_COUNT, max_kernels);
 }
 
 const char* prio3gpu_prof_kernel_name(int kid) {

@@ -169,8 +169,8 @@ def main():
     dt = (time.time() - t0) / args.steps
     kern = {}
     for v in (vl, vh):
-        ms, nl = (ctypes.c_double * 16)(), (ctypes.c_uint64 * 16)()
-        nk = L.prio3gpu_prof_read(v._ctx, ms, nl, 16)
+        ms, nl = (ctypes.c_double * 64)(), (ctypes.c_uint64 * 64)()
+        nk = min(64, L.prio3gpu_prof_read(v._ctx, ms, nl, 64))
         for i in range(nk):
             if nl[i]:
                 name = L.prio3gpu_prof_kernel_name(i).decode()
