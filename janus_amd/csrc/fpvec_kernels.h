@@ -364,29 +364,56 @@ __global__ void __launch_bounds__(256) k_fpv_wires0(Cfg cfg, uint32_t n, uint32_
   if (bad) atomicOr(&flags[r], FPV_BAD_ENCODING);
 }
 
-// grid (ceil(c1/256), n), 256 threads: wire1_j = C1[j] + sum_k L'_k z_((k-1) c1 + j), z decoded
-// from the n bits of the entry (Horner from the top bit, mod p).
+// grid (ceil(c1/256), n), 256 threads: wire1_j = C1[j] + sum_k L'_k z_((k-1) c1 + j) with
+// z_e = sum_l 2^l x_(n e + l) (the entry decoded from its n bits).  Linearity moves the decoding
+// into the weights: sum_k L'_k z_e = sum_k sum_l (2^l L'_k) x_(ne+l), so each bit is one lazily
+// reduced MAC against a weight from an LDS table 2^l L'_k (built per k-chunk by doubling) -- n
+// independent MACs per entry instead of a 2n-long serial double-and-add chain.
+constexpr uint32_t kW1Tab = 4096;  // table entries (64 KiB) per k-chunk
+
 __global__ void __launch_bounds__(256) k_fpv_wires1(Cfg cfg, uint32_t n, CRows meas, CRows wrows,
                                                     Rows prep, const uint8_t* status) {
   using FO = Field128Ops;
+  __shared__ F128 tab[kW1Tab];
   const uint32_t r = blockIdx.y;
-  if (r >= n || status[r] != ST_OK) return;
+  if (r >= n || status[r] != ST_OK) return;  // block-uniform
   const uint32_t c = cfg.chunk1, nb = cfg.bits;
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= c) return;
   const FpvW W = fpv_w_layout(cfg);
   const uint8_t* xr = meas.at(r);
   const uint8_t* wr = wrows.at(r);
+  const uint32_t kc = kW1Tab / nb;  // calls per table fill
   Wide acc;
   wide_zero(acc);
-  for (uint32_t k = 1; k <= cfg.calls1; ++k) {
-    const uint32_t e = (k - 1) * c + j;
-    if (e >= cfg.length) break;
-    const uint8_t* xe = xr + (size_t)e * nb * 16u;
-    F128 z = FO::zero();
-    for (int l = (int)nb - 1; l >= 0; --l) z = FO::add(FO::dbl(z), FO::load(xe + (size_t)l * 16u));
-    wide_mac(acc, FO::load(wr + (size_t)(W.l1 + k - 1) * 16u), z);
+  for (uint32_t k0 = 1; k0 <= cfg.calls1; k0 += kc) {
+    const uint32_t k1 = min(cfg.calls1 + 1u, k0 + kc);
+    __syncthreads();  // the previous chunk's table is no longer read
+    for (uint32_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
+      F128 w = FO::load(wr + (size_t)(W.l1 + k - 1) * 16u);  // L'_k (Montgomery)
+      F128* t = tab + (size_t)(k - k0) * nb;
+      for (uint32_t l = 0; l < nb; ++l) {
+        t[l] = w;
+        w = FO::dbl(w);
+      }
+    }
+    __syncthreads();
+    if (j < c) {
+      for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t e = (k - 1) * c + j;
+        if (e >= cfg.length) break;
+        const uint8_t* xe = xr + (size_t)e * nb * 16u;
+        const F128* t = tab + (size_t)(k - k0) * nb;
+        for (uint32_t l0 = 0; l0 < nb; l0 += 8) {
+          F128 xb[8];
+#pragma unroll
+          for (uint32_t u = 0; u < 8; ++u) xb[u] = FO::load(xe + (size_t)(l0 + u) * 16u);
+#pragma unroll
+          for (uint32_t u = 0; u < 8; ++u) wide_mac(acc, t[l0 + u], xb[u]);
+        }
+      }
+    }
   }
+  if (j >= c) return;
   const F128 w = FO::add(FO::load(wr + (size_t)(W.c1 + j) * 16u), wide_reduce(acc));
   FO::store(prep.at(r) + (size_t)(1 + cfg.arity + 1 + j) * 16u, w);
 }
