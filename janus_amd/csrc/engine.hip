@@ -186,6 +186,13 @@ struct prio3gpu_ctx {
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
   bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
   bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
+  uint32_t hx_cwave = 1;     // k_helper_xof consumer wave (1..3; PRIO3GPU_HX_CWAVE)
+  size_t hx_lds = 0;         // tuning: dynamic LDS per k_helper_xof block (PRIO3GPU_HX_LDS)
+  // Latency-bound sponge launches with fewer waves than CUs (FixedPoint: a few thousand reports)
+  // take one CU per workgroup: the dispatcher otherwise packs several workgroups, and the two
+  // contexts' kernels, onto shared SIMDs (config E: helper XOF 2.47 s -> 1.60 s per step).
+  bool spread = true;        // PRIO3GPU_SPREAD=0 disables
+  uint32_t cus = 0;          // compute units of the device
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
@@ -497,6 +504,10 @@ int copy_out(prio3gpu_ctx* c, void* dst, const void* dev_src, size_t bytes) {
 
 dim3 grid1(size_t n, uint32_t tpb) { return dim3((unsigned)((n + tpb - 1) / tpb)); }
 
+// Dynamic LDS that leaves no room for a second workgroup on the CU (160 KB each).
+constexpr size_t kSpreadLds = 96 * 1024;
+bool spread_ok(const prio3gpu_ctx* c, uint32_t blocks) { return c->spread && blocks <= c->cus; }
+
 // Measurement-share words that k_jr absorbs through its LDS window ("fast" blocks 1..lf cover
 // words [16, 21 (lf+1) - 5)); elements [e0, e1) lie entirely inside.  Field128 types with JR only.
 bool spec_range(const Cfg& g, uint32_t& nd, uint32_t& e0, uint32_t& e1) {
@@ -591,11 +602,14 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
         HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
         {
           PROF(KID_HELPER_XOF);
-          hipLaunchKernelGGL(k_helper_xof, dim3((N + kHxRows - 1) / kHxRows), dim3(2 * kHxRows), 0,
+          hipLaunchKernelGGL(k_helper_xof, dim3((N + kHxRows - 1) / kHxRows),
+                             dim3((c->hx_cwave + 1) * kHxRows),
+                             c->hx_lds ? std::min<size_t>(c->hx_lds, kSpreadLds)
+                                       : (spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0),
                              c->stream, g, N,
                              CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
-                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb);
+                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb, c->hx_cwave);
         }
         uint32_t h_fb = 0;
         HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -639,8 +653,13 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
   if (g.jr_len > 0) {
     {
       PROF(KID_JR);
-      const size_t jr_lds = std::max<size_t>((TPB / 64) * kJrWaveLds, std::min<size_t>(c->jr_lds, 160 * 1024));
-      hipLaunchKernelGGL(k_jr<FO>, grid1(n, TPB), dim3(TPB), jr_lds, c->stream, g, N,
+      // a wave per CU when there are few (see spread_ok); otherwise 4-wave blocks
+      const bool sp = c->jr_lds == 0 && spread_ok(c, (N + 63) / 64);
+      const uint32_t tpb = sp ? 64u : TPB;
+      const size_t jr_lds = sp ? kSpreadLds
+                               : std::max<size_t>((TPB / 64) * kJrWaveLds,
+                                                  std::min<size_t>(c->jr_lds, 160 * 1024));
+      hipLaunchKernelGGL(k_jr<FO>, grid1(n, tpb), dim3(tpb), jr_lds, c->stream, g, N,
                          (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
                          Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status,
                          spec_lo, spec_cy);
@@ -1049,12 +1068,24 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   auto* c = new prio3gpu_ctx();
   if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
   if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) c->fused_helper = fh[0] != '0';
+  if (const char* cw = getenv("PRIO3GPU_HX_CWAVE")) {
+    const int v = atoi(cw);
+    if (v >= 1 && v <= 3) c->hx_cwave = (uint32_t)v;
+  }
   if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
     const long v = strtol(ws, nullptr, 10);
     if (v >= 64 && v <= 1024) c->wires_slots = (uint32_t)v;
   }
   if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
+  if (const char* hl = getenv("PRIO3GPU_HX_LDS")) c->hx_lds = strtoull(hl, nullptr, 10);
+  if (const char* sp = getenv("PRIO3GPU_SPREAD")) c->spread = sp[0] != '0';
+  {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+      cu = 0;  // unknown: no spreading
+    c->cus = (uint32_t)cu;
+  }
   // Test switch: every XOF squeeze takes the exact per-element rejection path (the fast path's
   // bulk stores are skipped), and the FixedPoint helper runs its exact two-pass XOF.
   const char* ex = getenv("PRIO3GPU_EXACT_SQUEEZE");

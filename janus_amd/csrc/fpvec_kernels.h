@@ -48,17 +48,20 @@ namespace p3g {
 constexpr uint32_t kHxRows = 64;              // reports per workgroup (1 producer + 1 consumer wave)
 constexpr uint32_t kHxSlot = 21 * kHxRows;    // u64 words per LDS slot (word-major, row-minor)
 
-__global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
+__global__ void __launch_bounds__(4 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
                                                     CRows nonces, CRows public_shares,
                                                     Rows out_meas, Rows out_proof, Rows out_part,
                                                     Rows out_seed, Rows out_jr,
-                                                    const uint8_t* status, uint32_t* fallback) {
+                                                    const uint8_t* status, uint32_t* fallback,
+                                                    uint32_t cwave) {
   using FO = Field128Ops;
   __shared__ uint64_t ring[2 * kHxSlot];
   // wave 0 produces, wave 1 consumes (measured: 2 producer + 2 consumer waves per workgroup
   // ran 9 % slower)
   const uint32_t lane = threadIdx.x & (kHxRows - 1u);
-  const bool producer = threadIdx.x < kHxRows;  // wave-uniform role
+  const uint32_t wave = threadIdx.x / kHxRows;
+  const bool producer = wave == 0u;  // wave-uniform roles; other waves only join the barriers
+  const bool consumer = wave == cwave;
   const uint32_t r0 = blockIdx.x * kHxRows;
   const uint32_t r = r0 + lane;
   const bool live = r < n && (!status || status[r] == ST_OK);
@@ -123,7 +126,7 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
           }
         }
       }
-    } else if (i >= 1) {
+    } else if (consumer && i >= 1) {
       const int64_t b = i - 1;
       const uint64_t* slot = ring + (b & 1) * kHxSlot;
       const bool data = 21 * b < nd;  // else the block is past the share: zeros
@@ -154,7 +157,7 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
 #pragma unroll
       for (int k = 0; k < 6; ++k) carry[k] = data ? slot[(15 + k) * kHxRows + lane] : 0ull;
     }
-    const bool perm = producer ? (21 * (i + 1) < nd) : (i >= 1);
+    const bool perm = producer ? (21 * (i + 1) < nd) : (consumer && i >= 1);
     if (perm) keccak_x(s, cfg.xof);
     __syncthreads();
   }
@@ -166,7 +169,7 @@ __global__ void __launch_bounds__(2 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
     }
     return;
   }
-  if (!live) return;
+  if (!consumer || !live) return;
   const uint64_t plo = s[0], phi = s[1];
   st64(out_part.at(r), plo);
   st64(out_part.at(r) + 8, phi);
