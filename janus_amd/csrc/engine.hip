@@ -140,7 +140,7 @@ enum KernelId {
   KID_FLP_WIRES, KID_FPV_WEIGHTS, KID_FPV_WIRES0, KID_FPV_WIRES1, KID_FPV_FINAL, KID_DECIDE,
   KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
   KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
-  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM,
+  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM, KID_JR_RING,
   KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
@@ -148,7 +148,8 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_flp_wires", "k_fpv_weights", "k_fpv_wires0", "k_fpv_wires1", "k_fpv_finalize", "k_decide",
     "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
     "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
-    "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave", "k_shard_norm"};
+    "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave", "k_shard_norm",
+    "k_jr_ring"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -186,12 +187,12 @@ struct prio3gpu_ctx {
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
   bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
   bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
-  uint32_t hx_cwave = 1;     // k_helper_xof consumer wave (1..3; PRIO3GPU_HX_CWAVE)
   size_t hx_lds = 0;         // tuning: dynamic LDS per k_helper_xof block (PRIO3GPU_HX_LDS)
   // Latency-bound sponge launches with fewer waves than CUs (FixedPoint: a few thousand reports)
   // take one CU per workgroup: the dispatcher otherwise packs several workgroups, and the two
   // contexts' kernels, onto shared SIMDs (config E: helper XOF 2.47 s -> 1.60 s per step).
   bool spread = true;        // PRIO3GPU_SPREAD=0 disables
+  bool jr_ring = true;       // FixedPoint joint-rand part via k_jr_ring (PRIO3GPU_JR_RING=0: k_jr)
   uint32_t cus = 0;          // compute units of the device
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
@@ -603,13 +604,13 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
         {
           PROF(KID_HELPER_XOF);
           hipLaunchKernelGGL(k_helper_xof, dim3((N + kHxRows - 1) / kHxRows),
-                             dim3((c->hx_cwave + 1) * kHxRows),
+                             dim3(3 * kHxRows),
                              c->hx_lds ? std::min<size_t>(c->hx_lds, kSpreadLds)
                                        : (spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0),
                              c->stream, g, N,
                              CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
-                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb, c->hx_cwave);
+                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb);
         }
         uint32_t h_fb = 0;
         HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -650,7 +651,20 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     st->spec_e0 = se0;
     st->spec_e1 = se1;
   }
-  if (g.jr_len > 0) {
+  bool ring_done = false;
+  if constexpr (FO::ES == 16) {
+    // few huge FixedPoint reports: sponge wave + loader wave per CU (k_jr_ring)
+    if (g.jr_len > 0 && g.kind == KIND_FPVEC && c->jr_ring && c->jr_lds == 0 &&
+        spread_ok(c, (N + 63) / 64)) {
+      PROF(KID_JR_RING);
+      hipLaunchKernelGGL(k_jr_ring, dim3((N + 63) / 64), dim3(2 * kHxRows), kSpreadLds, c->stream,
+                         g, N, (uint32_t)st->agg_id, nonces, pub, blinds, meas,
+                         Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
+                         Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, spec_lo, spec_cy);
+      ring_done = true;
+    }
+  }
+  if (g.jr_len > 0 && !ring_done) {
     {
       PROF(KID_JR);
       // a wave per CU when there are few (see spread_ok); otherwise 4-wave blocks
@@ -1068,10 +1082,6 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   auto* c = new prio3gpu_ctx();
   if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
   if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) c->fused_helper = fh[0] != '0';
-  if (const char* cw = getenv("PRIO3GPU_HX_CWAVE")) {
-    const int v = atoi(cw);
-    if (v >= 1 && v <= 3) c->hx_cwave = (uint32_t)v;
-  }
   if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
     const long v = strtol(ws, nullptr, 10);
@@ -1080,6 +1090,7 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
   if (const char* hl = getenv("PRIO3GPU_HX_LDS")) c->hx_lds = strtoull(hl, nullptr, 10);
   if (const char* sp = getenv("PRIO3GPU_SPREAD")) c->spread = sp[0] != '0';
+  if (const char* jg = getenv("PRIO3GPU_JR_RING")) c->jr_ring = jg[0] != '0';
   {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)

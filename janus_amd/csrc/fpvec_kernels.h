@@ -33,8 +33,7 @@ namespace p3g {
 // only a few waves in flight the step is their latency.  Run one after the other (k_expand, then
 // k_jr) they cost two chains; here a 2-wave workgroup runs them as a producer/consumer pipeline:
 // producer waves squeeze block i of the expansion (store it, and hand it over through an LDS
-// double buffer) while consumer waves absorb block i - 1 into the joint-rand sponge, one
-// s_barrier per step.
+// ring of kHxDepth slots) while consumer waves absorb earlier blocks into the joint-rand sponge.
 // Both waves run the SAME permutation code on their own state (one hot Keccak copy: two would
 // not fit the instruction cache; a two-state single wave measured 20 % slower than serial).
 //
@@ -45,31 +44,76 @@ namespace p3g {
 // non-canonical element bumps `fallback`; the engine then re-runs the exact k_expand + k_jr for
 // the batch, so outputs are identical either way.
 // ------------------------------------------------------------------------------------------------
+// Absorb block b of a joint-rand-part message  header(blind) || agg_id || nonce || share  into
+// s, given share words [21b, 21b + 16) (A; zeros past the share) and carry = share words
+// [21b - 6, 21b) (for b = 0: carry[5] = the nonce's high word).  The 42-byte prefix puts share
+// word j at message bytes 42 + 8j, so message word w of block b is the 16-bit shifted pair
+// (D[21b + w - 6] >> 48) | (D[21b + w - 5] << 16).
+DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[16], int64_t b,
+                     int64_t nblocks, int64_t padw, uint64_t padv, const Cfg& cfg,
+                     uint32_t agg_id, const uint8_t* blind, const uint8_t* nonce) {
+#pragma unroll
+  for (int w = 0; w < 21; ++w) {
+    uint64_t v;
+    if (b == 0 && w < 5) {  // prefix: header(blind) || agg_id || nonce
+      MsgBlock m;
+      m.clear();
+      m.header(cfg.algo_id, DST_JOINT_RAND_PART, ld64(blind), ld64(blind + 8));
+      m.put8(25, agg_id);
+      m.put64(26, ld64(nonce));
+      m.put64(34, carry[5]);
+      v = m.w[w];
+    } else {
+      const uint64_t dlo = w <= 5 ? carry[w] : A[w - 6];
+      const uint64_t dhi = w <= 4 ? carry[w + 1] : A[w - 5];
+      v = (dlo >> 48) | (dhi << 16);
+    }
+    const int64_t g = 21 * b + w;
+    if (padw == g) v ^= padv;
+    if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
+    s[w] ^= v;
+  }
+}
+
 constexpr uint32_t kHxRows = 64;              // reports per workgroup (1 producer + 1 consumer wave)
 constexpr uint32_t kHxSlot = 21 * kHxRows;    // u64 words per LDS slot (word-major, row-minor)
+constexpr uint32_t kHxDepth = 4;              // ring slots: the producer may run 4 blocks ahead
 
-__global__ void __launch_bounds__(4 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
+__global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
                                                     CRows nonces, CRows public_shares,
                                                     Rows out_meas, Rows out_proof, Rows out_part,
                                                     Rows out_seed, Rows out_jr,
-                                                    const uint8_t* status, uint32_t* fallback,
-                                                    uint32_t cwave) {
+                                                    const uint8_t* status, uint32_t* fallback) {
   using FO = Field128Ops;
-  __shared__ uint64_t ring[2 * kHxSlot];
-  // wave 0 produces, wave 1 consumes (measured: 2 producer + 2 consumer waves per workgroup
-  // ran 9 % slower)
+  __shared__ uint64_t ring[kHxDepth * kHxSlot];
+  // Ring handoff through two LDS counters instead of a per-block s_barrier: the producer
+  // publishes `produced` after its slot writes have landed (lgkmcnt(0)); the consumer publishes
+  // `consumed` after its slot reads have returned.  Neither wave waits for the other's
+  // permutation unless the ring is full / empty, so each runs at its own pace.
+  __shared__ uint32_t produced, consumed, stored;
+  volatile uint32_t* vprod = &produced;
+  volatile uint32_t* vcons = &consumed;
+  volatile uint32_t* vstor = &stored;
+  if (threadIdx.x == 0) {
+    produced = 0u;
+    consumed = 0u;
+    stored = 0u;
+  }
+  __syncthreads();
+  // wave 0 produces, wave 1 consumes, wave 2 stores the expanded share to HBM (measured: 2
+  // producer + 2 consumer waves per workgroup ran 9 % slower)
   const uint32_t lane = threadIdx.x & (kHxRows - 1u);
-  const uint32_t wave = threadIdx.x / kHxRows;
-  const bool producer = wave == 0u;  // wave-uniform roles; other waves only join the barriers
-  const bool consumer = wave == cwave;
+  const uint32_t wave = threadIdx.x / kHxRows;  // wave-uniform roles
+  const bool producer = wave == 0u, storer = wave == 2u;
   const uint32_t r0 = blockIdx.x * kHxRows;
   const uint32_t r = r0 + lane;
   const bool live = r < n && (!status || status[r] == ST_OK);
-  const uint32_t rr = r < n ? r : n - 1u;  // every lane runs the loop (barriers), clamped row
+  const uint32_t rr = r < n ? r : n - 1u;  // every lane runs the loop, clamped row
   const uint8_t* hs = helper_shares.at(rr);
   const int64_t nd = (int64_t)cfg.meas_len * 2;    // meas-share words
   const int64_t total = 42 + 8 * nd;                // consumer's message bytes before padding
   const int64_t nblocks = total / 168 + 1;          // consumer blocks
+  const int64_t nprod = (nd + 20) / 21;             // producer blocks
   const int64_t padw = total >> 3;
   const uint64_t padv = (uint64_t)cfg.xof.pad << ((total & 7) * 8);
   const uint64_t nonce_hi = ld64(nonces.at(rr) + 8);
@@ -91,91 +135,251 @@ __global__ void __launch_bounds__(4 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
   carry[5] = nonce_hi;
   bool bad = false;
   uint8_t* om = out_meas.at(rr);
-  for (int64_t i = 0; i <= nblocks; ++i) {
+  // One loop for all roles so the waves share ONE inlined permutation (two copies would not
+  // fit the instruction cache).
+  const int64_t iters = producer || storer ? nprod : nblocks;
+  for (int64_t i = 0; i < iters; ++i) {
+    bool perm = true;
     if (producer) {
       const int64_t j0 = 21 * i;
-      if (j0 < nd) {
-        uint64_t* slot = ring + (i & 1) * kHxSlot;
-        if (j0 + 21 <= nd) {  // whole block: 16-B stores (block i starts 16-B aligned iff i even)
-          if (live) {
-            uint8_t* o = om + 8 * j0;
-            if ((i & 1) == 0) {
+      while (i - (int64_t)min(*vcons, *vstor) >= (int64_t)kHxDepth) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+      uint64_t* slot = ring + (i % kHxDepth) * kHxSlot;
 #pragma unroll
-              for (int w = 0; w < 20; w += 2)
-                *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
-              st64(o + 160, s[20]);
-            } else {
-              st64(o, s[0]);
+      for (int w = 0; w < 21; ++w) slot[w * kHxRows + lane] = j0 + w < nd ? s[w] : 0ull;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
+      *vprod = (uint32_t)(i + 1);
+      perm = 21 * (i + 1) < nd;
+    } else if (storer) {
+      // store block i of the expanded share and check its elements are canonical
+      const int64_t j0 = 21 * i;
+      while ((int64_t)*vprod <= i) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+      const uint64_t* slot = ring + (i % kHxDepth) * kHxSlot;
 #pragma unroll
-              for (int w = 1; w < 21; w += 2)
-                *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
-            }
-          }
+      for (int w = 0; w < 21; ++w) s[w] = slot[w * kHxRows + lane];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
+      *vstor = (uint32_t)(i + 1);
+      if (j0 + 21 <= nd) {  // whole block: 16-B stores (block i starts 16-B aligned iff i even)
+        if (live) {
+          uint8_t* o = om + 8 * j0;
+          if ((i & 1) == 0) {
 #pragma unroll
-          for (int w = 0; w < 21; ++w) {
-            if (((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
-            slot[w * kHxRows + lane] = s[w];
-          }
-        } else {
+            for (int w = 0; w < 20; w += 2)
+              *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
+            st64(o + 160, s[20]);
+          } else {
+            st64(o, s[0]);
 #pragma unroll
-          for (int w = 0; w < 21; ++w) {
-            const bool in = j0 + w < nd;
-            if (in && live) st64(om + 8 * (j0 + w), s[w]);
-            if (in && ((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
-            slot[w * kHxRows + lane] = in ? s[w] : 0ull;
+            for (int w = 1; w < 21; w += 2)
+              *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
           }
         }
+#pragma unroll
+        for (int w = 0; w < 21; ++w)
+          if (((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
+      } else {
+#pragma unroll
+        for (int w = 0; w < 21; ++w) {
+          const bool in = j0 + w < nd;
+          if (in && live) st64(om + 8 * (j0 + w), s[w]);
+          if (in && ((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
+        }
       }
-    } else if (consumer && i >= 1) {
-      const int64_t b = i - 1;
-      const uint64_t* slot = ring + (b & 1) * kHxSlot;
+      perm = false;
+    } else {
+      const int64_t b = i;
       const bool data = 21 * b < nd;  // else the block is past the share: zeros
       uint64_t A[16];
+      if (data) {
+        while ((int64_t)*vprod <= b) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        const uint64_t* slot = ring + (b % kHxDepth) * kHxSlot;
 #pragma unroll
-      for (int w = 0; w < 16; ++w) A[w] = data ? slot[w * kHxRows + lane] : 0ull;
+        for (int w = 0; w < 16; ++w) A[w] = slot[w * kHxRows + lane];
+      } else {
 #pragma unroll
-      for (int w = 0; w < 21; ++w) {
-        uint64_t v;
-        if (b == 0 && w < 5) {  // prefix: header(blind) || [1] || nonce
-          MsgBlock m;
-          m.clear();
-          m.header(cfg.algo_id, DST_JOINT_RAND_PART, ld64(hs + 32), ld64(hs + 40));
-          m.put8(25, 1u);
-          m.put64(26, ld64(nonces.at(rr)));
-          m.put64(34, nonce_hi);
-          v = m.w[w];
-        } else {
-          const uint64_t dlo = w <= 5 ? carry[w] : A[w - 6];
-          const uint64_t dhi = w <= 4 ? carry[w + 1] : A[w - 5];
-          v = (dlo >> 48) | (dhi << 16);
-        }
-        const int64_t g = 21 * b + w;
-        if (padw == g) v ^= padv;
-        if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
-        s[w] ^= v;
+        for (int w = 0; w < 16; ++w) A[w] = 0ull;
       }
+      jrp_absorb(s, carry, A, b, nblocks, padw, padv, cfg, 1u, hs + 32, nonces.at(rr));
+      if (data) {
+        const uint64_t* slot = ring + (b % kHxDepth) * kHxSlot;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) carry[k] = data ? slot[(15 + k) * kHxRows + lane] : 0ull;
+        for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kHxRows + lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
+        *vcons = (uint32_t)(b + 1);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) carry[k] = 0ull;
+      }
     }
-    const bool perm = producer ? (21 * (i + 1) < nd) : (consumer && i >= 1);
     if (perm) keccak_x(s, cfg.xof);
-    __syncthreads();
+  }
+  if (storer) {
+    if (live && bad) atomicAdd(fallback, 1u);
+    return;
   }
   if (producer) {
     if (live) {
-      if (bad) atomicAdd(fallback, 1u);
       xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), 1u,
                                  cfg.proof_len, out_proof.at(r), cfg.xof, cfg.exact_squeeze);
     }
     return;
   }
-  if (!consumer || !live) return;
+  if (!live) return;
   const uint64_t plo = s[0], phi = s[1];
   st64(out_part.at(r), plo);
   st64(out_part.at(r) + 8, phi);
   const uint8_t* ps = public_shares.at(r);
   uint64_t slo, shi;
   derive_jr_seed(cfg.xof, cfg.algo_id, ld64(ps), ld64(ps + 8), plo, phi, slo, shi);
+  st64(out_seed.at(r), slo);
+  st64(out_seed.at(r) + 8, shi);
+  MsgBlock m;
+  m.clear();
+  m.header(cfg.algo_id, DST_JOINT_RANDOMNESS, slo, shi);
+  m.pad(25, cfg.xof);
+  uint64_t s2[25];
+  sponge_one_block(s2, m, cfg.xof);
+  squeeze_vec<FO>(s2, cfg.jr_len, out_jr.at(r), cfg.xof, cfg.exact_squeeze);
+}
+
+// Joint-rand part of an aggregator's own (given) measurement share for few, huge reports
+// (k_jr_ring; the leader side of config E): k_jr's sponge wave stalls on its LDS-DMA window
+// refills and does the speculative column sums itself.  Here a loader wave streams share blocks
+// from HBM into an LDS ring (the same counter handoff as k_helper_xof) and writes the
+// speculative column sums k_accum_spec consumes (every share word, same layout and row clamp as
+// k_jr), while the sponge wave only absorbs and permutes.  Ring rows are 65 words apart so the
+// loader's column reads (lane = word) hit distinct banks.
+constexpr uint32_t kJrRingStride = kHxRows + 1;
+
+__global__ void __launch_bounds__(2 * kHxRows) k_jr_ring(Cfg cfg, uint32_t n, uint32_t agg_id,
+                                                 CRows nonces, CRows public_shares,
+                                                 CRows blinds, CRows meas, Rows out_part,
+                                                 Rows out_seed, Rows out_jr,
+                                                 const uint8_t* status, uint64_t* spec_lo,
+                                                 uint8_t* spec_cy) {
+  using FO = Field128Ops;
+  constexpr uint32_t kSlot = 21 * kJrRingStride;
+  __shared__ uint64_t ring[kHxDepth * kSlot];
+  __shared__ uint32_t produced, consumed;
+  volatile uint32_t* vprod = &produced;
+  volatile uint32_t* vcons = &consumed;
+  if (threadIdx.x == 0) {
+    produced = 0u;
+    consumed = 0u;
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & (kHxRows - 1u);
+  const bool loader = threadIdx.x >= kHxRows;  // wave 0: sponge, wave 1: loader
+  const uint32_t r0 = blockIdx.x * kHxRows;
+  const uint32_t r = r0 + lane;
+  const bool live = r < n && (!status || status[r] == ST_OK);
+  const uint32_t rr = r < n ? r : n - 1u;  // rows past n: the last row (k_jr's clamp)
+  const uint8_t* data = meas.at(rr);
+  const int64_t nd = (int64_t)cfg.meas_len * 2;  // share words
+  const int64_t total = 42 + 8 * nd;
+  const int64_t nblocks = total / 168 + 1;
+  const int64_t nprod = (nd + 20) / 21;
+  const int64_t padw = total >> 3;
+  const uint64_t padv = (uint64_t)cfg.xof.pad << ((total & 7) * 8);
+  uint64_t s[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) s[i] = 0ull;
+  uint64_t carry[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) carry[i] = 0ull;
+  carry[5] = ld64(nonces.at(rr) + 8);
+  const int64_t iters = loader ? nprod : nblocks;
+  for (int64_t i = 0; i < iters; ++i) {
+    bool perm = true;
+    if (loader) {
+      const int64_t j0 = 21 * i;
+      const uint8_t* src = data + 8 * j0;  // loads first: in flight while the ring is full
+      if (j0 + 21 <= nd) {  // whole block: 16-B loads (block i starts 16-B aligned iff i even)
+        if ((i & 1) == 0) {
+#pragma unroll
+          for (int w = 0; w < 20; w += 2) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src + 8 * w);
+            s[w] = v.x;
+            s[w + 1] = v.y;
+          }
+          s[20] = ld64(src + 160);
+        } else {
+          s[0] = ld64(src);
+#pragma unroll
+          for (int w = 1; w < 21; w += 2) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src + 8 * w);
+            s[w] = v.x;
+            s[w + 1] = v.y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int w = 0; w < 21; ++w) s[w] = j0 + w < nd ? ld64(src + 8 * w) : 0ull;
+      }
+      while (i - (int64_t)*vcons >= (int64_t)kHxDepth) __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+      uint64_t* slot = ring + (i % kHxDepth) * kSlot;
+#pragma unroll
+      for (int w = 0; w < 21; ++w) slot[w * kJrRingStride + lane] = s[w];
+      if (spec_lo != nullptr && lane < 21u && j0 + lane < nd) {
+        // column sum of word j0 + lane over the wave's 64 rows (this wave's own LDS writes
+        // above complete first: one wave's LDS operations execute in order)
+        const uint64_t* col = slot + lane * kJrRingStride;
+        uint32_t l32 = 0, h32 = 0, cy = 0;
+#pragma unroll 16
+        for (int k = 0; k < 64; ++k) acc_u64(l32, h32, cy, col[k]);
+        const size_t at = (size_t)(r0 >> 6) * (size_t)nd + (size_t)(j0 + lane);
+        spec_lo[at] = ((uint64_t)h32 << 32) | l32;
+        spec_cy[at] = (uint8_t)cy;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
+      *vprod = (uint32_t)(i + 1);
+      perm = false;
+    } else {
+      const int64_t b = i;
+      const bool has = 21 * b < nd;  // else the block is past the share: zeros
+      uint64_t A[16];
+      if (has) {
+        while ((int64_t)*vprod <= b) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        const uint64_t* slot = ring + (b % kHxDepth) * kSlot;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) A[w] = slot[w * kJrRingStride + lane];
+      } else {
+#pragma unroll
+        for (int w = 0; w < 16; ++w) A[w] = 0ull;
+      }
+      jrp_absorb(s, carry, A, b, nblocks, padw, padv, cfg, agg_id, blinds.at(rr), nonces.at(rr));
+      if (has) {
+        const uint64_t* slot = ring + (b % kHxDepth) * kSlot;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kJrRingStride + lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
+        *vcons = (uint32_t)(b + 1);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) carry[k] = 0ull;
+      }
+    }
+    if (perm) keccak_x(s, cfg.xof);
+  }
+  if (loader || !live) return;
+  const uint64_t plo = s[0], phi = s[1];
+  st64(out_part.at(r), plo);
+  st64(out_part.at(r) + 8, phi);
+  const uint8_t* ps = public_shares.at(r);
+  uint64_t p0lo = ld64(ps), p0hi = ld64(ps + 8), p1lo = ld64(ps + 16), p1hi = ld64(ps + 24);
+  if (agg_id == 0) {
+    p0lo = plo;
+    p0hi = phi;
+  } else {
+    p1lo = plo;
+    p1hi = phi;
+  }
+  uint64_t slo, shi;
+  derive_jr_seed(cfg.xof, cfg.algo_id, p0lo, p0hi, p1lo, p1hi, slo, shi);
   st64(out_seed.at(r), slo);
   st64(out_seed.at(r) + 8, shi);
   MsgBlock m;

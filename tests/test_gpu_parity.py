@@ -361,6 +361,33 @@ def test_fpvec_helper_two_pass_path_bit_exact(name, monkeypatch):
     np.testing.assert_array_equal(ho, b.helper_out)
 
 
+@pytest.mark.parametrize("env", [{}, {"PRIO3GPU_JR_RING": "0"}, {"PRIO3GPU_SPREAD": "0"}],
+                         ids=["ring", "k_jr_spread", "k_jr_packed"])
+@pytest.mark.parametrize("name", ["fp16_3", "fp16_300"])
+def test_fpvec_leader_jr_variants(name, env, monkeypatch):
+    """The leader's FixedPoint joint-rand part runs k_jr_ring (sponge wave + loader wave writing
+    the speculative column sums) when few waves fit one per CU, else k_jr.  Every variant gives
+    the oracle's prep shares, and its column sums fold into the exact aggregate with a rejected
+    row subtracted (report 1's status set before prepare_next; rows past n are clamped copies)."""
+    for k, val in env.items():
+        monkeypatch.setenv(k, val)
+    b = batch(name)
+    v = gpu_vdaf(b)
+    ls = v.new_state(0, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    assert (lst == 0).all()
+    np.testing.assert_array_equal(lp, b.leader_prep)
+    lst = lst.copy()
+    lst[1] = 5
+    lagg = v.new_aggregate(1)
+    v.prepare_next(ls, b.prep_msg, lst, want_output_shares=False, agg=lagg)
+    got, cnt = lagg.read(0)
+    slots = np.zeros(b.n, np.uint32)
+    slots[1] = 1
+    exp, ecnt = expected_aggregate(b, "leader", slots=slots, slot=0)
+    assert got == exp and cnt == ecnt == b.n - 1
+
+
 def test_report_checksum_and_interval():
     """Accumulator::update's per-batch bookkeeping next to the aggregate share: ReportIdChecksum
     = XOR of SHA-256(report id) (core/src/report_id.rs:18-44, hashlib as the oracle) and the
