@@ -187,6 +187,8 @@ struct prio3gpu_ctx {
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
   bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
   bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
+  bool fused_helper_all = false;  // A/B: every Field128 type's helper via k_helper_xof (=2)
+  uint32_t hx_depth = 2;          // A/B: ring depth of that variant (PRIO3GPU_HX_DEPTH=4)
   size_t hx_lds = 0;         // tuning: dynamic LDS per k_helper_xof block (PRIO3GPU_HX_LDS)
   // Latency-bound sponge launches with fewer waves than CUs (FixedPoint: a few thousand reports)
   // take one CU per workgroup: the dispatcher otherwise packs several workgroups, and the two
@@ -196,6 +198,7 @@ struct prio3gpu_ctx {
   uint32_t cus = 0;          // compute units of the device
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
+  uint32_t wires_rows = 0;     // >0: k_flp_wires_lds with this many share rows per LDS chunk
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
@@ -586,55 +589,6 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     hipLaunchKernelGGL(k_query_rand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N, vk_lo, vk_hi,
                        nonces, t_rows, d_status);
   }
-  CRows meas, proof, blinds;
-  if (st->agg_id == 0) {
-    meas = CRows{d_in, g.leader_share_len};
-    proof = CRows{d_in + (size_t)g.meas_len * es, g.leader_share_len};
-    blinds = CRows{d_in + (size_t)(g.meas_len + g.proof_len) * es, g.leader_share_len};
-  } else {
-    Rows mo{st->meas.u8(), (size_t)g.meas_len * es};
-    Rows po{st->proof.u8(), (size_t)g.proof_len * es};
-    bool fused_done = false;
-    if constexpr (FO::ES == 16) {
-      // Few huge reports: the two helper sponges (expansion, joint-rand part) in lockstep.
-      if (g.kind == KIND_FPVEC && c->fused_helper && g.jr_len > 0) {
-        CHK(c->fallback.ensure(4));
-        uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
-        HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
-        {
-          PROF(KID_HELPER_XOF);
-          hipLaunchKernelGGL(k_helper_xof, dim3((N + kHxRows - 1) / kHxRows),
-                             dim3(3 * kHxRows),
-                             c->hx_lds ? std::min<size_t>(c->hx_lds, kSpreadLds)
-                                       : (spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0),
-                             c->stream, g, N,
-                             CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
-                             Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
-                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb);
-        }
-        uint32_t h_fb = 0;
-        HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        fused_done = h_fb == 0;  // else: a non-canonical element; redo the exact two-pass path
-      }
-    }
-    if (fused_done) {
-      st->spec_ok = false;
-      st->meas_rows = CRows{mo.base, mo.stride};
-      st->proof_rows = CRows{po.base, po.stride};
-      st->n = n;
-      st->xof_done = true;
-      return 0;
-    }
-    {
-      PROF(KID_EXPAND);
-      hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
-                         (uint32_t)st->agg_id, CRows{d_in, g.helper_share_len}, mo, po, d_status);
-    }
-    meas = CRows{mo.base, mo.stride};
-    proof = CRows{po.base, po.stride};
-    blinds = CRows{d_in + 32, g.helper_share_len};
-  }
   st->spec_ok = false;
   uint64_t* spec_lo = nullptr;
   uint8_t* spec_cy = nullptr;
@@ -650,6 +604,57 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     st->spec_nd = snd;
     st->spec_e0 = se0;
     st->spec_e1 = se1;
+  }
+  CRows meas, proof, blinds;
+  if (st->agg_id == 0) {
+    meas = CRows{d_in, g.leader_share_len};
+    proof = CRows{d_in + (size_t)g.meas_len * es, g.leader_share_len};
+    blinds = CRows{d_in + (size_t)(g.meas_len + g.proof_len) * es, g.leader_share_len};
+  } else {
+    Rows mo{st->meas.u8(), (size_t)g.meas_len * es};
+    Rows po{st->proof.u8(), (size_t)g.proof_len * es};
+    bool fused_done = false;
+    if constexpr (FO::ES == 16) {
+      // Few huge reports: the two helper sponges (expansion, joint-rand part) in lockstep.
+      if ((g.kind == KIND_FPVEC || c->fused_helper_all) && c->fused_helper && g.jr_len > 0) {
+        CHK(c->fallback.ensure(4));
+        uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
+        HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
+        {
+          PROF(KID_HELPER_XOF);
+          auto kern = (g.kind == KIND_FPVEC || c->hx_depth == 4) ? k_helper_xof<kHxDepth>
+                                                                   : k_helper_xof<2>;
+          hipLaunchKernelGGL(kern, dim3((N + kHxRows - 1) / kHxRows),
+                             dim3(3 * kHxRows),
+                             c->hx_lds ? std::min<size_t>(c->hx_lds, kSpreadLds)
+                                       : (spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0),
+                             c->stream, g, N,
+                             CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
+                             Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
+                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb,
+                             spec_lo, spec_cy);
+        }
+        uint32_t h_fb = 0;
+        HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        fused_done = h_fb == 0;  // else: a non-canonical element; redo the exact two-pass path
+      }
+    }
+    if (fused_done) {  // the storer wave wrote the speculative column sums
+      st->meas_rows = CRows{mo.base, mo.stride};
+      st->proof_rows = CRows{po.base, po.stride};
+      st->n = n;
+      st->xof_done = true;
+      return 0;
+    }
+    {
+      PROF(KID_EXPAND);
+      hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
+                         (uint32_t)st->agg_id, CRows{d_in, g.helper_share_len}, mo, po, d_status);
+    }
+    meas = CRows{mo.base, mo.stride};
+    proof = CRows{po.base, po.stride};
+    blinds = CRows{d_in + 32, g.helper_share_len};
   }
   bool ring_done = false;
   if constexpr (FO::ES == 16) {
@@ -767,9 +772,25 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
     size_t lds2 = esz * (2 * (size_t)g.calls + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
     lds2 = (lds2 + 15) & ~(size_t)15;
     PROF(KID_FLP_WIRES);
-    hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
-                       wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                       Rows{st->prep.u8(), g.prep_share_len}, d_status);
+    if (FO::ES == 16 && c->wires_rows > 0 && nthr <= 256) {
+      // share through an LDS ring, R rows per chunk (a multiple of the row groups)
+      const uint32_t R = ((std::max(c->wires_rows, dims.H) + dims.H - 1) / dims.H) * dims.H;
+      const size_t chunk = (size_t)R * dims.cols * 16;
+      const size_t tail = 16 * (2 * (size_t)dims.H * dims.cols + nthr) + 16;
+      const size_t lds3 = std::max(2 * chunk, tail) + 32 * (size_t)g.calls;
+      if (lds3 > 64 * 1024) {
+        set_err("k_flp_wires_lds: %zu B of LDS", lds3);
+        return PRIO3GPU_E_ARG;
+      }
+      if constexpr (FO::ES == 16)
+        hipLaunchKernelGGL(k_flp_wires_lds<FO>, dim3(N), dim3(nthr), lds3, c->stream, g, N, dims,
+                           R, meas, wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                           Rows{st->prep.u8(), g.prep_share_len}, d_status);
+    } else {
+      hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
+                         wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
+    }
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -1081,16 +1102,24 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   HIPCHK(hipSetDevice(device));
   auto* c = new prio3gpu_ctx();
   if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
-  if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) c->fused_helper = fh[0] != '0';
+  if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) {
+    c->fused_helper = fh[0] != '0';
+    c->fused_helper_all = fh[0] == '2';
+  }
   if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
     const long v = strtol(ws, nullptr, 10);
     if (v >= 64 && v <= 1024) c->wires_slots = (uint32_t)v;
   }
+  if (const char* wr = getenv("PRIO3GPU_WIRES_LDS")) {
+    const long v = strtol(wr, nullptr, 10);
+    if (v >= 0 && v <= 64) c->wires_rows = (uint32_t)v;
+  }
   if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
   if (const char* hl = getenv("PRIO3GPU_HX_LDS")) c->hx_lds = strtoull(hl, nullptr, 10);
   if (const char* sp = getenv("PRIO3GPU_SPREAD")) c->spread = sp[0] != '0';
   if (const char* jg = getenv("PRIO3GPU_JR_RING")) c->jr_ring = jg[0] != '0';
+  if (const char* hd = getenv("PRIO3GPU_HX_DEPTH")) c->hx_depth = hd[0] == '4' ? 4u : 2u;
   {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)

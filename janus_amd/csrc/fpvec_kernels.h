@@ -76,16 +76,20 @@ DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[1
 }
 
 constexpr uint32_t kHxRows = 64;              // reports per workgroup (1 producer + 1 consumer wave)
-constexpr uint32_t kHxSlot = 21 * kHxRows;    // u64 words per LDS slot (word-major, row-minor)
 constexpr uint32_t kHxDepth = 4;              // ring slots: the producer may run 4 blocks ahead
 
+template <uint32_t kDepth>
 __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
                                                     CRows nonces, CRows public_shares,
                                                     Rows out_meas, Rows out_proof, Rows out_part,
                                                     Rows out_seed, Rows out_jr,
-                                                    const uint8_t* status, uint32_t* fallback) {
+                                                    const uint8_t* status, uint32_t* fallback,
+                                                    uint64_t* spec_lo, uint8_t* spec_cy) {
   using FO = Field128Ops;
-  __shared__ uint64_t ring[kHxDepth * kHxSlot];
+  // slot rows are kHxRows + 1 words apart: the storer's column reads (words x rows) hit distinct
+  // banks; the producer's and consumer's row accesses stay conflict-free
+  constexpr uint32_t kStride = kHxRows + 1, kSlot = 21 * kStride;
+  __shared__ uint64_t ring[kDepth * kSlot];
   // Ring handoff through two LDS counters instead of a per-block s_barrier: the producer
   // publishes `produced` after its slot writes have landed (lgkmcnt(0)); the consumer publishes
   // `consumed` after its slot reads have returned.  Neither wave waits for the other's
@@ -142,11 +146,11 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
     bool perm = true;
     if (producer) {
       const int64_t j0 = 21 * i;
-      while (i - (int64_t)min(*vcons, *vstor) >= (int64_t)kHxDepth) __builtin_amdgcn_s_sleep(1);
+      while (i - (int64_t)min(*vcons, *vstor) >= (int64_t)kDepth) __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
-      uint64_t* slot = ring + (i % kHxDepth) * kHxSlot;
+      uint64_t* slot = ring + (i % kDepth) * kSlot;
 #pragma unroll
-      for (int w = 0; w < 21; ++w) slot[w * kHxRows + lane] = j0 + w < nd ? s[w] : 0ull;
+      for (int w = 0; w < 21; ++w) slot[w * kStride + lane] = j0 + w < nd ? s[w] : 0ull;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
       *vprod = (uint32_t)(i + 1);
       perm = 21 * (i + 1) < nd;
@@ -155,13 +159,45 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
       const int64_t j0 = 21 * i;
       while ((int64_t)*vprod <= i) __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
-      const uint64_t* slot = ring + (i % kHxDepth) * kHxSlot;
+      const uint64_t* slot = ring + (i % kDepth) * kSlot;
 #pragma unroll
-      for (int w = 0; w < 21; ++w) s[w] = slot[w * kHxRows + lane];
+      for (int w = 0; w < 21; ++w) s[w] = slot[w * kStride + lane];
+      // speculative accumulation (k_jr's layout): column sums of the block's 21 words over the
+      // wave's 64 rows, lane = word wc + 21 gq summing rows gq, gq + 3, ... (lane 63 idle)
+      const uint32_t gq = lane / 21u, wc = lane - 21u * gq;
+      uint64_t xs[22];
+      if (spec_lo != nullptr) {
+        const uint64_t* col = slot + (gq < 3u ? wc : 0u) * kStride;
+#pragma unroll
+        for (int k = 0; k < 22; ++k) {
+          const uint32_t row = gq + 3u * (uint32_t)k;
+          xs[k] = (gq < 3u && row < 64u) ? col[row] : 0ull;
+        }
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
       *vstor = (uint32_t)(i + 1);
+      if (spec_lo != nullptr) {
+        uint32_t l32 = 0, h32 = 0, cy = 0;
+#pragma unroll
+        for (int k = 0; k < 22; ++k) acc_u64(l32, h32, cy, xs[k]);
+        const uint32_t s1 = (lane + 21u) & 63u, s2 = (lane + 42u) & 63u;
+        const uint32_t la = __shfl(l32, (int)s1, 64), ha = __shfl(h32, (int)s1, 64);
+        const uint32_t ca = __shfl(cy, (int)s1, 64);
+        const uint32_t lb = __shfl(l32, (int)s2, 64), hb = __shfl(h32, (int)s2, 64);
+        const uint32_t cb = __shfl(cy, (int)s2, 64);
+        if (lane < 21u && j0 + lane < nd) {
+          acc_u64(l32, h32, cy, ((uint64_t)ha << 32) | la);
+          acc_u64(l32, h32, cy, ((uint64_t)hb << 32) | lb);
+          const size_t at = (size_t)(r0 >> 6) * (size_t)nd + (size_t)(j0 + lane);
+          spec_lo[at] = ((uint64_t)h32 << 32) | l32;
+          spec_cy[at] = (uint8_t)(cy + ca + cb);
+        }
+      }
+      // every row below n is stored (also reports rejected before this kernel): k_accum_spec
+      // subtracts a rejected row's stored words from the column sums, which include it
+      const bool st_row = spec_lo != nullptr ? r < n : live;
       if (j0 + 21 <= nd) {  // whole block: 16-B stores (block i starts 16-B aligned iff i even)
-        if (live) {
+        if (st_row) {
           uint8_t* o = om + 8 * j0;
           if ((i & 1) == 0) {
 #pragma unroll
@@ -182,7 +218,7 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
 #pragma unroll
         for (int w = 0; w < 21; ++w) {
           const bool in = j0 + w < nd;
-          if (in && live) st64(om + 8 * (j0 + w), s[w]);
+          if (in && st_row) st64(om + 8 * (j0 + w), s[w]);
           if (in && ((j0 + w) & 1) && !hi_ok(s[w])) bad = true;
         }
       }
@@ -194,18 +230,18 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
       if (data) {
         while ((int64_t)*vprod <= b) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
-        const uint64_t* slot = ring + (b % kHxDepth) * kHxSlot;
+        const uint64_t* slot = ring + (b % kDepth) * kSlot;
 #pragma unroll
-        for (int w = 0; w < 16; ++w) A[w] = slot[w * kHxRows + lane];
+        for (int w = 0; w < 16; ++w) A[w] = slot[w * kStride + lane];
       } else {
 #pragma unroll
         for (int w = 0; w < 16; ++w) A[w] = 0ull;
       }
       jrp_absorb(s, carry, A, b, nblocks, padw, padv, cfg, 1u, hs + 32, nonces.at(rr));
       if (data) {
-        const uint64_t* slot = ring + (b % kHxDepth) * kHxSlot;
+        const uint64_t* slot = ring + (b % kDepth) * kSlot;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kHxRows + lane];
+        for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kStride + lane];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
         *vcons = (uint32_t)(b + 1);
       } else {
