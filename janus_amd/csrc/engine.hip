@@ -189,6 +189,7 @@ struct prio3gpu_ctx {
   bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
   bool fused_helper_all = false;  // A/B: every Field128 type's helper via k_helper_xof (=2)
   uint32_t hx_depth = 2;          // A/B: ring depth of that variant (PRIO3GPU_HX_DEPTH=4)
+  bool hx_spec = true;            // A/B: k_helper_xof's storer column sums (PRIO3GPU_HX_SPEC=0: off)
   size_t hx_lds = 0;         // tuning: dynamic LDS per k_helper_xof block (PRIO3GPU_HX_LDS)
   // Latency-bound sponge launches with fewer waves than CUs (FixedPoint: a few thousand reports)
   // take one CU per workgroup: the dispatcher otherwise packs several workgroups, and the two
@@ -198,7 +199,6 @@ struct prio3gpu_ctx {
   uint32_t cus = 0;          // compute units of the device
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
-  uint32_t wires_rows = 0;     // >0: k_flp_wires_lds with this many share rows per LDS chunk
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
@@ -632,7 +632,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
                              CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
                              Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb,
-                             spec_lo, spec_cy);
+                             c->hx_spec ? spec_lo : nullptr, spec_cy);
         }
         uint32_t h_fb = 0;
         HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -640,7 +640,8 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
         fused_done = h_fb == 0;  // else: a non-canonical element; redo the exact two-pass path
       }
     }
-    if (fused_done) {  // the storer wave wrote the speculative column sums
+    if (fused_done) {  // the storer wave wrote the speculative column sums (unless hx_spec is off)
+      if (!c->hx_spec) st->spec_ok = false;
       st->meas_rows = CRows{mo.base, mo.stride};
       st->proof_rows = CRows{po.base, po.stride};
       st->n = n;
@@ -772,25 +773,9 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
     size_t lds2 = esz * (2 * (size_t)g.calls + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
     lds2 = (lds2 + 15) & ~(size_t)15;
     PROF(KID_FLP_WIRES);
-    if (FO::ES == 16 && c->wires_rows > 0 && nthr <= 256) {
-      // share through an LDS ring, R rows per chunk (a multiple of the row groups)
-      const uint32_t R = ((std::max(c->wires_rows, dims.H) + dims.H - 1) / dims.H) * dims.H;
-      const size_t chunk = (size_t)R * dims.cols * 16;
-      const size_t tail = 16 * (2 * (size_t)dims.H * dims.cols + nthr) + 16;
-      const size_t lds3 = std::max(2 * chunk, tail) + 32 * (size_t)g.calls;
-      if (lds3 > 64 * 1024) {
-        set_err("k_flp_wires_lds: %zu B of LDS", lds3);
-        return PRIO3GPU_E_ARG;
-      }
-      if constexpr (FO::ES == 16)
-        hipLaunchKernelGGL(k_flp_wires_lds<FO>, dim3(N), dim3(nthr), lds3, c->stream, g, N, dims,
-                           R, meas, wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                           Rows{st->prep.u8(), g.prep_share_len}, d_status);
-    } else {
-      hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
-                         wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
-    }
+    hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
+                       wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                       Rows{st->prep.u8(), g.prep_share_len}, d_status);
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -1111,14 +1096,11 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
     const long v = strtol(ws, nullptr, 10);
     if (v >= 64 && v <= 1024) c->wires_slots = (uint32_t)v;
   }
-  if (const char* wr = getenv("PRIO3GPU_WIRES_LDS")) {
-    const long v = strtol(wr, nullptr, 10);
-    if (v >= 0 && v <= 64) c->wires_rows = (uint32_t)v;
-  }
   if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
   if (const char* hl = getenv("PRIO3GPU_HX_LDS")) c->hx_lds = strtoull(hl, nullptr, 10);
   if (const char* sp = getenv("PRIO3GPU_SPREAD")) c->spread = sp[0] != '0';
   if (const char* jg = getenv("PRIO3GPU_JR_RING")) c->jr_ring = jg[0] != '0';
+  if (const char* hs = getenv("PRIO3GPU_HX_SPEC")) c->hx_spec = hs[0] != '0';
   if (const char* hd = getenv("PRIO3GPU_HX_DEPTH")) c->hx_depth = hd[0] == '4' ? 4u : 2u;
   {
     int cu = 0;

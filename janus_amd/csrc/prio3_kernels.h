@@ -1415,113 +1415,6 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
   }
 }
 
-// The same wire pass with the measurement share streamed through LDS (Field128): the block's waves
-// copy chunks of `R` share rows (R * c elements, contiguous in HBM) into a two-slot LDS ring with
-// LDS-DMA (global_load_lds_dwordx4: no VGPRs held by loads in flight) one chunk ahead of the MACs,
-// which read their elements back with conflict-free ds_read_b128.  Thread (h, j) takes rows
-// h, h + H, ... of each chunk (R is a multiple of H).  LDS: ring[2][R c 16] | MM[C] | LM[C], and
-// PA/PB/RED reuse the ring after the last chunk.
-template <class FO>
-__global__ void __launch_bounds__(256) k_flp_wires_lds(Cfg cfg, uint32_t n, FlpDims dims,
-                                                       uint32_t R, CRows meas, WMat wm, CRows jr,
-                                                       Rows out_prep, uint8_t* status) {
-  using T = typename FO::T;
-  static_assert(FO::ES == 16, "Field128 only");
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t r = blockIdx.x;
-  if (r >= n) return;
-  if (status[r] != ST_OK) return;  // block-uniform
-  const uint32_t tid = threadIdx.x, nthr = blockDim.x, wave = tid >> 6, lane = tid & 63u;
-  const uint32_t nwaves = (nthr + 63u) >> 6;
-  const uint32_t C = cfg.calls, c = dims.cols, H = dims.H;
-  const uint32_t chunk_bytes = R * c * 16u;
-  uint8_t* ring = smem;
-  T* MM = reinterpret_cast<T*>(smem + 2u * chunk_bytes);
-  T* LM = MM + C;
-  for (uint32_t k = tid; k < 2 * C; k += nthr) MM[k] = FO::load(wm.el(r, k));
-  const uint8_t* xr = meas.at(r);
-  const uint32_t total = cfg.meas_len * 16u;
-  const uint32_t nchunks = (C + R - 1u) / R;
-  // chunk q -> ring slot q & 1: 1-KB pieces, piece p by wave p % nwaves (16 B per lane)
-  auto issue = [&](uint32_t q) {
-    const uint32_t base = q * chunk_bytes;
-    uint8_t* dst = ring + (q & 1u) * chunk_bytes;
-    const uint32_t len = min(chunk_bytes, total - base);
-    for (uint32_t p = wave; p * 1024u < len; p += nwaves) {
-      const uint32_t off = p * 1024u + lane * 16u;
-      if (off < len)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(xr + base + off),
-            (__attribute__((address_space(3))) void*)(dst + p * 1024u), 16, 0, 0);
-    }
-  };
-  issue(0);
-  const uint32_t slots = H * c;
-  const bool act = tid < slots;
-  const uint32_t j = act ? tid % c : 0u, h = act ? tid / c : 0u;
-  Wide wa, wb;
-  wide_zero(wa);
-  wide_zero(wb);
-  bool bad = false;
-  T xsum = FO::zero();
-  for (uint32_t q = 0; q < nchunks; ++q) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // chunk q in LDS (every wave's pieces); slot (q+1)&1 free (chunk q-1 done)
-    if (q + 1u < nchunks) issue(q + 1u);
-    if (act) {
-      const uint8_t* buf = ring + (q & 1u) * chunk_bytes;
-      const uint32_t k0 = q * R;
-      for (uint32_t kk = h; kk < R; kk += H) {
-        const uint32_t k = k0 + kk;
-        const uint32_t i = k * c + j;
-        if (k < C && i < cfg.meas_len) {
-          const T x = FO::load(buf + (size_t)(kk * c + j) * 16u);
-          bad |= !FO::is_canonical(x);
-          wide_mac(wa, MM[k], x);
-          wide_mac(wb, LM[k], x);
-          if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x);
-        }
-      }
-    }
-  }
-  __syncthreads();  // ring reads done: PA/PB/RED/flag reuse it
-  T* PA = reinterpret_cast<T*>(smem);
-  T* PB = PA + slots;
-  T* RED = PB + slots;
-  uint32_t* flag = reinterpret_cast<uint32_t*>(RED + nthr);
-  if (tid == 0) *flag = 0u;
-  if (act) {
-    PA[tid] = wide_reduce(wa);
-    PB[tid] = wide_reduce(wb);
-  }
-  __syncthreads();
-  uint8_t* outp = out_prep.at(r);
-  for (uint32_t jj = tid; jj < c; jj += nthr) {
-    T a = FO::zero(), b = FO::zero();
-    for (uint32_t hh = 0; hh < H; ++hh) {
-      a = FO::add(a, PA[hh * c + jj]);
-      b = FO::add(b, PB[hh * c + jj]);
-    }
-    const T rp = FO::load(wm.el(r, 2 * C + jj));  // Montgomery
-    const T w0 = FO::add(FO::load(wm.el(r, 2 * C + c + jj)), FO::mul(rp, a));
-    const T w1 = FO::add(FO::load(wm.el(r, 2 * C + 2 * c + jj)), b);
-    FO::store(outp + (size_t)(1 + 2 * jj) * 16u, w0);
-    FO::store(outp + (size_t)(2 + 2 * jj) * 16u, w1);
-  }
-  if (bad) atomicOr(flag, 1u);
-  if (cfg.kind == KIND_HISTOGRAM) xsum = block_sum<FO>(xsum, RED, tid, nthr);
-  __syncthreads();
-  if (tid == 0) {
-    if (cfg.kind == KIND_HISTOGRAM) {
-      const T gsum = FO::load(wm.el(r, 2 * C + 3 * c));
-      const T r1m = FO::to_mont(FO::load(jr.at(r) + 16));
-      const T sc = FO::sub(xsum, FO::half());
-      FO::store(outp, FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc)));
-    }
-    if (*flag & 1u) status[r] = ST_INVALID_MESSAGE;
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // prepare_shares_to_prepare_message (prio): verifier = sum of shares; decide; msg = derive_seed(
 // 0^16, dst6, part_0 || part_1).  decide: v == 0 and G(wires) == p(t),
