@@ -131,6 +131,27 @@ def perms_per_report(kind_name, sizes):
     }
 
 
+def leader_output_shares(leader_in, kind, bits, length, s, p):
+    """prio's truncate() of the leader's measurement share (the first MEAS elements of its input
+    share), exact integers: Count/Histogram keep the share, Sum/SumVec fold each entry's bits as
+    sum_b 2^b x_b mod p.  (n, OUT * ES) uint8."""
+    es = s.field_size
+    n = leader_in.shape[0]
+    m = leader_in[:, :s.meas_len * es].reshape(n, s.meas_len, es)
+    x = np.zeros((n, s.meas_len), dtype=object)
+    for k in range(es // 8):
+        x += m[:, :, 8 * k:8 * k + 8].copy().view("<u8").reshape(n, s.meas_len).astype(object) << (64 * k)
+    if kind in (1, 2):
+        nb = bits
+        x = x.reshape(n, -1, nb)
+        w = np.array([1 << b for b in range(nb)], dtype=object)
+        x = (x * w).sum(axis=2) % p
+    out = np.zeros((n, x.shape[1] * es), np.uint8)
+    for i in range(n):
+        out[i] = np.frombuffer(b"".join(int(v).to_bytes(es, "little") for v in x[i]), np.uint8)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -484,17 +505,35 @@ def main():
     gpub = d_pub[:G] if d_pub is not None else None
     glp, glst = gv.prepare_init(gls, d_nonces[:G], gpub, d_lin[:G])
     gmsgs, ghst = gv.helper_init(ghs, d_nonces[:G], gpub, d_hin[:G], glp, agg=ghagg)
-    gv.prepare_next(gls, gmsgs, glst, want_output_shares=False, agg=glagg)
-    ref_res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=False)
+    gout = gv.prepare_next(gls, gmsgs, glst, want_output_shares=True, agg=glagg)
+    if isinstance(gout, tuple):
+        gout = gout[0]
+    ref_res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=True)
     (gla, glc), (gha, ghc) = glagg.read(0), ghagg.read(0)
     assert glc == ghc == ref_res["count"] == G, (glc, ghc, ref_res["count"], G)
     assert gla == ref_res["agg_l"].tobytes(), "leader aggregate share != C restatement"
     assert gha == ref_res["agg_h"].tobytes(), "helper aggregate share != C restatement"
+    # sampled prep shares, prep messages and output shares byte-equal too
+    assert (ref_res["status"] == 0).all() and (glst == 0).all() and (ghst == 0).all()
+    assert np.array_equal(glp, ref_res["lprep"]), "leader prep shares != C restatement"
+    ghs2 = gv.new_state(1, G)
+    ghp, _ = gv.prepare_init(ghs2, d_nonces[:G], gpub, d_hin[:G])
+    ghs2.close()
+    assert np.array_equal(ghp, ref_res["hprep"]), "helper prep shares != C restatement"
+    if s.prep_msg:
+        assert np.array_equal(np.asarray(gmsgs)[:, :s.prep_msg], ref_res["msgs"]), \
+            "prep messages != C restatement"
+    no = min(G, 64)
+    assert np.array_equal(np.asarray(gout)[:no], leader_output_shares(cl[:no], kind, bits, length, s,
+                                                                      vdaf.modulus)), \
+        "leader output shares != truncate(leader measurement share)"
     for o in (gls, ghs, glagg, ghagg):
         o.close()
     parity = (f"aggregate-share bytes == C restatement (both aggregators, {G} reports/rank "
-              f"through the product path); unshard(aggregate) == plaintext sum over every timed "
-              f"step; report-ID checksums == hashlib; status all ok")
+              f"through the product path); leader and helper prep shares and prep messages of "
+              f"those {G} reports == C restatement; leader output shares of {no} == truncate(meas "
+              f"share); unshard(aggregate) == plaintext sum over every timed step; report-ID "
+              f"checksums == hashlib; status all ok")
 
     # ---- helper-only variant (the A1 path alone: helper_init + bookkeeping), SURVEY §8(d) -------
     helper_only = None
