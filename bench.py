@@ -152,6 +152,48 @@ def leader_output_shares(leader_in, kind, bits, length, s, p):
     return out
 
 
+def oracle_transcript_gate(vdaf, kind, bits, length, chunk, vk, syn, d_pub, d_lin, d_hin, n=2):
+    """XofTurboShake128 runs (no C restatement of that XOF): the first n synthetic reports through
+    the Python oracle's run_vdaf (VdafTranscript, core/src/test_util/mod.rs:87-233) vs the GPU's
+    client shard, both prep shares, prep messages and both output shares, byte for byte."""
+    from oracle import prio3 as O
+    ctor = {0: lambda: O.Prio3.new_count(), 1: lambda: O.Prio3.new_sum(bits),
+            2: lambda: O.Prio3.new_sum_vec(bits, length, chunk),
+            3: lambda: O.Prio3.new_histogram(length, chunk)}[kind]
+    ov = ctor()
+    ov.xof = O.XofTurboShake128
+    s = vdaf.sizes
+    rows = dict(public_share=d_pub, leader_input_share=d_lin, helper_input_share=d_hin)
+    want = {k: [] for k in ("leader_prep_share", "helper_prep_share", "prep_msg",
+                            "leader_out_share", "helper_out_share")}
+    for i in range(n):
+        nonce = syn["nonces"][i].tobytes()
+        m = [int(x) for x in syn["meas"][i]] if kind == 2 else int(syn["meas"][i][0])
+        t = O.run_vdaf(ov, vk, nonce, m, syn["rand"][i].tobytes())
+        for k, d in rows.items():
+            if d is not None:
+                assert d[i].cpu().numpy().tobytes() == t[k], f"GPU shard != oracle {k}"
+        for k in want:
+            want[k].append(t[k])
+    nz = syn["nonces"][:n]
+    pub = d_pub[:n].cpu().numpy() if d_pub is not None else None
+    ls, hs = vdaf.new_state(0, n), vdaf.new_state(1, n)
+    lp, lst = vdaf.prepare_init(ls, nz, pub, d_lin[:n].cpu().numpy())
+    hp, hst = vdaf.prepare_init(hs, nz, pub, d_hin[:n].cpu().numpy())
+    msgs, st = vdaf.prepare_shares_to_prepare_message(lp, hp)
+    lo, lst = vdaf.prepare_next(ls, msgs, lst.copy())
+    ho, hst = vdaf.prepare_next(hs, msgs, hst.copy())
+    assert (lst == 0).all() and (hst == 0).all() and (st == 0).all()
+    got = dict(leader_prep_share=lp, helper_prep_share=hp, prep_msg=np.asarray(msgs)[:, :s.prep_msg],
+               leader_out_share=lo, helper_out_share=ho)
+    for k, rows_ in want.items():
+        assert np.asarray(got[k]).tobytes() == b"".join(rows_), f"GPU {k} != oracle"
+    ls.close()
+    hs.close()
+    return (f"first {n} reports: GPU client shard, prep shares, prep messages and output shares "
+            f"== Python oracle run_vdaf (XofTurboShake128)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,6 +213,10 @@ def main():
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--xof", default="shake128", choices=["shake128", "turboshake128"],
+                    help="XofShake128 (prio 0.15.1 / VDAF-07: the reference's XOF, the metric) or "
+                         "XofTurboShake128 (VDAF-08+, the north star's Keccak-p[1600,12]; the C "
+                         "restatement is SHAKE128-only, so its gates use the Python oracle)")
     ap.add_argument("--workers", type=int, default=1,
                     help="concurrent aggregation-job workers per GPU, one engine context (HIP "
                          "stream) and one contiguous slice of the batch each (Janus "
@@ -197,7 +243,7 @@ def main():
     from janus_amd import _lib
     from janus_amd._lib import check, lib
     from janus_amd.parallel import shard_range
-    from janus_amd.prio3 import Comm, Prio3Gpu
+    from janus_amd.prio3 import XOF_SHAKE128, XOF_TURBOSHAKE128, Comm, Prio3Gpu
     from oracle.ref import Prio3Ref
 
     kind, bits, length, chunk, label = CONFIGS[args.config]
@@ -210,8 +256,10 @@ def main():
     vk = hashlib.shake_128(b"verify-key" + cfg_id).digest(16)
 
     W = max(1, args.workers)
-    vdafs = [Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=local_rank)
-             for _ in range(W)]
+    turbo = args.xof == "turboshake128"
+    xof_id = XOF_TURBOSHAKE128 if turbo else XOF_SHAKE128
+    vdafs = [Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=local_rank,
+                      xof=xof_id) for _ in range(W)]
     vdaf = vdafs[0]
     s = vdaf.sizes
 
@@ -237,12 +285,16 @@ def main():
     del d_rand
     gen_s = time.time() - t0
     U = min(U, B)  # CPU-baseline sample size
-    chk = ref.gen(cfg_id, lo, min(U, 64), threads=args.gen_threads)
-    k = chk["nonces"].shape[0]
-    assert np.array_equal(d_lin[:k].cpu().numpy(), chk["leader_in"]), "GPU shard != C shard"
-    assert np.array_equal(d_hin[:k].cpu().numpy(), chk["helper_in"]), "GPU shard != C shard"
-    if s.public_share:
-        assert np.array_equal(d_pub[:k].cpu().numpy(), chk["public"]), "GPU shard != C shard"
+    if turbo:
+        turbo_gate = oracle_transcript_gate(vdaf, kind, bits, length, chunk, vk, syn, d_pub, d_lin,
+                                            d_hin, n=2)
+    else:
+        chk = ref.gen(cfg_id, lo, min(U, 64), threads=args.gen_threads)
+        k = chk["nonces"].shape[0]
+        assert np.array_equal(d_lin[:k].cpu().numpy(), chk["leader_in"]), "GPU shard != C shard"
+        assert np.array_equal(d_hin[:k].cpu().numpy(), chk["helper_in"]), "GPU shard != C shard"
+        if s.public_share:
+            assert np.array_equal(d_pub[:k].cpu().numpy(), chk["public"]), "GPU shard != C shard"
     d_lprep = torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
     d_hprep = (torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev) if args.overlap
                else None)
@@ -275,7 +327,7 @@ def main():
         # --overlap: the helper gets its own context (HIP stream), so its prepare_init runs
         # concurrently with the leader's, like two aggregator processes sharing the GPU
         wk.hv = (Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk,
-                          device=local_rank) if args.overlap else wk.v)
+                          device=local_rank, xof=xof_id) if args.overlap else wk.v)
         wk.ls, wk.hs = wk.v.new_state(0, wk.n), wk.hv.new_state(1, wk.n)
         wk.lagg, wk.hagg = wk.v.new_aggregate(1), wk.hv.new_aggregate(1)
         wk.lpart, wk.hpart = ((wk.v.new_aggregate(1), wk.hv.new_aggregate(1)) if world > 1
@@ -495,45 +547,50 @@ def main():
     # restatement of prio 0.15.1: both aggregators' aggregate-share bytes and counts identical.
     G = min(U, B)
     nthr = cpu_threads(args.cpu_threads)
-    cn = d_nonces[:G].cpu().numpy()
-    cp = d_pub[:G].cpu().numpy() if d_pub is not None else np.zeros((G, 0), np.uint8)
-    cl = d_lin[:G].cpu().numpy()
-    ch = d_hin[:G].cpu().numpy()
-    gv = workers[0].v
-    gls, ghs = gv.new_state(0, G), gv.new_state(1, G)
-    glagg, ghagg = gv.new_aggregate(1), gv.new_aggregate(1)
-    gpub = d_pub[:G] if d_pub is not None else None
-    glp, glst = gv.prepare_init(gls, d_nonces[:G], gpub, d_lin[:G])
-    gmsgs, ghst = gv.helper_init(ghs, d_nonces[:G], gpub, d_hin[:G], glp, agg=ghagg)
-    gout = gv.prepare_next(gls, gmsgs, glst, want_output_shares=True, agg=glagg)
-    if isinstance(gout, tuple):
-        gout = gout[0]
-    ref_res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=True)
-    (gla, glc), (gha, ghc) = glagg.read(0), ghagg.read(0)
-    assert glc == ghc == ref_res["count"] == G, (glc, ghc, ref_res["count"], G)
-    assert gla == ref_res["agg_l"].tobytes(), "leader aggregate share != C restatement"
-    assert gha == ref_res["agg_h"].tobytes(), "helper aggregate share != C restatement"
-    # sampled prep shares, prep messages and output shares byte-equal too
-    assert (ref_res["status"] == 0).all() and (glst == 0).all() and (ghst == 0).all()
-    assert np.array_equal(glp, ref_res["lprep"]), "leader prep shares != C restatement"
-    ghs2 = gv.new_state(1, G)
-    ghp, _ = gv.prepare_init(ghs2, d_nonces[:G], gpub, d_hin[:G])
-    ghs2.close()
-    assert np.array_equal(ghp, ref_res["hprep"]), "helper prep shares != C restatement"
-    if s.prep_msg:
-        assert np.array_equal(np.asarray(gmsgs)[:, :s.prep_msg], ref_res["msgs"]), \
-            "prep messages != C restatement"
-    no = min(G, 64)
-    assert np.array_equal(np.asarray(gout)[:no], leader_output_shares(cl[:no], kind, bits, length, s,
-                                                                      vdaf.modulus)), \
-        "leader output shares != truncate(leader measurement share)"
-    for o in (gls, ghs, glagg, ghagg):
-        o.close()
-    parity = (f"aggregate-share bytes == C restatement (both aggregators, {G} reports/rank "
-              f"through the product path); leader and helper prep shares and prep messages of "
-              f"those {G} reports == C restatement; leader output shares of {no} == truncate(meas "
-              f"share); unshard(aggregate) == plaintext sum over every timed step; report-ID "
-              f"checksums == hashlib; status all ok")
+    if turbo:  # the C restatement is SHAKE128-only: the Python-oracle transcript gate above
+        parity = (f"{turbo_gate}; unshard(aggregate) == plaintext sum over every timed step; "
+                  f"report-ID checksums == hashlib; status all ok (XofTurboShake128: parity "
+                  f"unpinned beyond the oracle)")
+    else:
+        cn = d_nonces[:G].cpu().numpy()
+        cp = d_pub[:G].cpu().numpy() if d_pub is not None else np.zeros((G, 0), np.uint8)
+        cl = d_lin[:G].cpu().numpy()
+        ch = d_hin[:G].cpu().numpy()
+        gv = workers[0].v
+        gls, ghs = gv.new_state(0, G), gv.new_state(1, G)
+        glagg, ghagg = gv.new_aggregate(1), gv.new_aggregate(1)
+        gpub = d_pub[:G] if d_pub is not None else None
+        glp, glst = gv.prepare_init(gls, d_nonces[:G], gpub, d_lin[:G])
+        gmsgs, ghst = gv.helper_init(ghs, d_nonces[:G], gpub, d_hin[:G], glp, agg=ghagg)
+        gout = gv.prepare_next(gls, gmsgs, glst, want_output_shares=True, agg=glagg)
+        if isinstance(gout, tuple):
+            gout = gout[0]
+        ref_res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=True)
+        (gla, glc), (gha, ghc) = glagg.read(0), ghagg.read(0)
+        assert glc == ghc == ref_res["count"] == G, (glc, ghc, ref_res["count"], G)
+        assert gla == ref_res["agg_l"].tobytes(), "leader aggregate share != C restatement"
+        assert gha == ref_res["agg_h"].tobytes(), "helper aggregate share != C restatement"
+        # sampled prep shares, prep messages and output shares byte-equal too
+        assert (ref_res["status"] == 0).all() and (glst == 0).all() and (ghst == 0).all()
+        assert np.array_equal(glp, ref_res["lprep"]), "leader prep shares != C restatement"
+        ghs2 = gv.new_state(1, G)
+        ghp, _ = gv.prepare_init(ghs2, d_nonces[:G], gpub, d_hin[:G])
+        ghs2.close()
+        assert np.array_equal(ghp, ref_res["hprep"]), "helper prep shares != C restatement"
+        if s.prep_msg:
+            assert np.array_equal(np.asarray(gmsgs)[:, :s.prep_msg], ref_res["msgs"]), \
+                "prep messages != C restatement"
+        no = min(G, 64)
+        assert np.array_equal(np.asarray(gout)[:no], leader_output_shares(cl[:no], kind, bits, length, s,
+                                                                          vdaf.modulus)), \
+            "leader output shares != truncate(leader measurement share)"
+        for o in (gls, ghs, glagg, ghagg):
+            o.close()
+        parity = (f"aggregate-share bytes == C restatement (both aggregators, {G} reports/rank "
+                  f"through the product path); leader and helper prep shares and prep messages of "
+                  f"those {G} reports == C restatement; leader output shares of {no} == truncate(meas "
+                  f"share); unshard(aggregate) == plaintext sum over every timed step; report-ID "
+                  f"checksums == hashlib; status all ok")
 
     # ---- helper-only variant (the A1 path alone: helper_init + bookkeeping), SURVEY §8(d) -------
     helper_only = None
@@ -578,20 +635,26 @@ def main():
     avg_launch_s = dms / 1e3 / dlaunch
     # B / W reports per launch; k_jr runs once per aggregator and worker (2 W launches per step)
     nlaunch = bounds[1] - bounds[0]
-    pmc = load_pmc(args.config)
+    # the PMC passes profile the SHAKE128 build of the command; a TurboSHAKE128 permutation is the
+    # last 12 of Keccak-f's 24 rounds: half the ops, twice the measured ceiling rate
+    pmc = load_pmc(args.config) if not turbo else {}
+    rf = 0.5 if turbo else 1.0
     if dname in perms and perms[dname]:
-        ops = perms[dname] * nlaunch * OPS_PER_PERM
+        ops = perms[dname] * nlaunch * OPS_PER_PERM * rf
         achieved = ops / avg_launch_s / 1e12
         perm_rate = perms[dname] * nlaunch / avg_launch_s
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
                 "kernel": dname, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                "model": f"{perms[dname]} Keccak-f[1600]/report x {OPS_PER_PERM} int32 ops "
-                         f"(SURVEY §8(d)) x {nlaunch} reports/launch",
+                "model": (f"{perms[dname]} Keccak-f[1600]/report x {OPS_PER_PERM} int32 ops "
+                          f"(SURVEY §8(d)) x {nlaunch} reports/launch" if not turbo else
+                          f"{perms[dname]} Keccak-p[1600,12]/report x {OPS_PER_PERM // 2} int32 "
+                          f"ops (half of SURVEY §8(d)'s 24-round figure) x {nlaunch} "
+                          f"reports/launch"),
                 "keccak_perms_per_s": round(perm_rate, 1),
                 # vs the measured register-only Keccak-f ceiling of this chip (tools/mb_keccak_occ.hip)
-                "keccak_ceiling_perms_per_s": KECCAK_CEILING,
-                "keccak_ceiling_frac": round(perm_rate / KECCAK_CEILING, 4),
+                "keccak_ceiling_perms_per_s": KECCAK_CEILING / rf,
+                "keccak_ceiling_frac": round(perm_rate * rf / KECCAK_CEILING, 4),
                 "algorithmic_hbm_bytes_per_launch": (
                     nlaunch * s.meas_len * s.field_size if dname == "k_jr" else
                     nlaunch * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand"
@@ -628,7 +691,7 @@ def main():
 
     # ---- CPU baseline: C restatement of prio 0.15.1, bounded sample, rank 0 at N = 1 -----------
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_baseline:
+    if rank == 0 and world == 1 and args.cpu_baseline and not turbo:
         done, t0 = 0, time.perf_counter()
         while True:
             res = ref.prepare_batch(cn, cp, cl, ch, threads=nthr, outputs=False)
@@ -701,7 +764,9 @@ def main():
                     "note": "CPU stage in front of the GPU path (north star); not in `value`"}
 
     out = {
-        "metric": METRIC if args.config == "sumvec" else f"reports/sec prepared+aggregated, {label}",
+        "metric": (METRIC if args.config == "sumvec" and not turbo else
+                   f"reports/sec prepared+aggregated, {label}" + (", XofTurboShake128" if turbo
+                                                                  else "")),
         "value": round(value, 2),
         "unit": "reports/s",
         "n_gpus": world,
@@ -714,7 +779,8 @@ def main():
         "dtype": "u128 (Field128 mod p)" if s.field_size == 16 else "u64 (Field64 mod p)",
         "data": f"synthetic: {B} distinct reports/GPU (SURVEY §8(d) recipe; shares made by the GPU "
                 f"client shard), resident in HBM",
-        "config": {"workload": label, "reports_per_gpu_per_step": B, "job_workers_per_gpu": W,
+        "config": {"workload": label, "xof": "XofTurboShake128" if turbo else "XofShake128",
+                   "reports_per_gpu_per_step": B, "job_workers_per_gpu": W,
                    "parallelism": f"report-sharded x{world}, {W} job stream(s)/GPU, "
                                   f"RCCL all-gather merge"},
         "roofline": roof,
