@@ -140,7 +140,7 @@ enum KernelId {
   KID_FLP_WIRES, KID_FPV_WEIGHTS, KID_FPV_WIRES0, KID_FPV_WIRES1, KID_FPV_FINAL, KID_DECIDE,
   KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
   KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
-  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM, KID_JR_RING,
+  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM, KID_JR_RING, KID_FLP_QUERY_LANE,
   KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
@@ -149,7 +149,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
     "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
     "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave", "k_shard_norm",
-    "k_jr_ring"};
+    "k_jr_ring", "k_flp_query_lane"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -197,6 +197,7 @@ struct prio3gpu_ctx {
   bool spread = true;        // PRIO3GPU_SPREAD=0 disables
   bool jr_ring = true;       // FixedPoint joint-rand part via k_jr_ring (PRIO3GPU_JR_RING=0: k_jr)
   uint32_t cus = 0;          // compute units of the device
+  bool flp_query_lane = true;    // Count/Sum: k_flp_query_lane; PRIO3GPU_FLPQ_BLOCK=1: k_flp_query
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
@@ -762,6 +763,11 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
                        CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                        CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
                        wrows);
+  } else if ((g.kind == KIND_COUNT || g.kind == KIND_SUM) && c->flp_query_lane) {
+    PROF(KID_FLP_QUERY_LANE);
+    hipLaunchKernelGGL(k_flp_query_lane<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, meas,
+                       proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status);
   } else {
     PROF(KID_FLP_QUERY);
     hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr1), lds, c->stream, g, N, d1, meas, proof,
@@ -1091,6 +1097,7 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
     c->fused_helper = fh[0] != '0';
     c->fused_helper_all = fh[0] == '2';
   }
+  if (const char* fq = getenv("PRIO3GPU_FLPQ_BLOCK")) c->flp_query_lane = fq[0] == '0';
   if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
     const long v = strtol(ws, nullptr, 10);

@@ -917,6 +917,135 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
 }
 
 // ------------------------------------------------------------------------------------------------
+// FLP query for Count (Mul, 1 call) and Sum (PolyEval(x^2 - x), `bits` calls), one LANE per report:
+// registers only, no LDS, no barriers, no NTT.  With L_k(t) = (t^m - 1)/m * alpha^k / (t - alpha^k):
+//   wire_w(t) = C * sum_{k=0..calls} a_{w,k} / (t - alpha^k),   C = (t^m - 1)/m,
+//     a_{w,0} = proof seed s_w,  a_{w,k} = alpha^k * (input of call k on wire w)
+//   Sum:   v = sum_{k=1..calls} r^k p(alpha^k) = sum_{i<m} F_i G(r alpha^i),
+//          F = the gadget poly folded mod x^m - 1,  G(y) = sum_{k=1..calls} y^k
+//            = y (y^calls - 1)/(y - 1)  (= calls if y == 1),  y^calls = r^calls alpha^(i calls mod m)
+//   Count: v = p(alpha) - x_0
+//   p(t) by Horner.
+// Both sums of fractions are accumulated as one numerator / denominator pair (N d + a D, D d: three
+// multiplications per term), and the two denominators share ONE inversion (Montgomery's trick), so
+// Sum32 costs ~900 multiplications per report where the block kernel ran two size-64 NTTs across
+// 64 threads with a barrier per stage.  A zero t - alpha^k means t^m == 1: VdafPrepError (prio's
+// "root of unity" rejection); the values computed then are discarded.
+// ------------------------------------------------------------------------------------------------
+template <class FO>
+DEVI typename FO::T inv_mont(const typename FO::T& x) {
+  if constexpr (FO::ES == 16) return inv_mont128(x);
+  else return mont_pow<FO>(x, Field64Ops::P - 2ull);
+}
+
+template <class FO>
+__global__ void __launch_bounds__(256) k_flp_query_lane(Cfg cfg, uint32_t n, CRows meas,
+                                                        CRows proof, CRows tq, CRows jr,
+                                                        CRows part, Rows out_prep,
+                                                        uint8_t* status) {
+  using T = typename FO::T;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (status[r] != ST_OK) return;
+  const size_t ES = FO::ES;
+  const uint32_t m = cfg.m, calls = cfg.calls, arity = cfg.arity, gp_len = cfg.gp_len;
+  const uint8_t* xr = meas.at(r);
+  const uint8_t* pr = proof.at(r);
+  const uint8_t* gp = pr + (size_t)arity * ES;  // gadget poly coefficients
+  bool bad = false;
+  const T one = FO::one_mont();
+  const T tm = FO::to_mont(FO::load(tq.at(r)));
+  T tmm = tm;
+  for (uint32_t i = 0; i < cfg.logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
+  const bool root = FO::eq(tmm, one);
+  const T cm = FO::mul(FO::sub(tmm, one), ld_tw<FO>(cfg, m));  // (t^m - 1)/m, Montgomery
+
+  // wires: N_w / D over k = 0..calls
+  T nw0 = FO::zero(), nw1 = FO::zero(), dw = one;
+  const T s0 = FO::load(pr), s1 = arity > 1 ? FO::load(pr + ES) : FO::zero();
+  bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
+  T x0 = FO::zero();
+  if (cfg.kind == KIND_COUNT) {
+    x0 = FO::load(xr);
+    bad |= !FO::is_canonical(x0);
+  }
+  for (uint32_t k = 0; k <= calls; ++k) {
+    const T ak = ld_tw<FO>(cfg, k);  // alpha^k, Montgomery
+    const T d = FO::sub(tm, ak);
+    T a0, a1;
+    if (k == 0) {
+      a0 = s0;
+      a1 = s1;
+    } else {
+      T x = x0;
+      if (cfg.kind != KIND_COUNT) {
+        x = FO::load(xr + (size_t)(k - 1) * ES);
+        bad |= !FO::is_canonical(x);
+      }
+      a0 = FO::mul(ak, x);
+      a1 = a0;
+    }
+    nw0 = FO::add(FO::mul(nw0, d), FO::mul(a0, dw));
+    if (arity > 1) nw1 = FO::add(FO::mul(nw1, d), FO::mul(a1, dw));
+    dw = FO::mul(dw, d);
+  }
+
+  // p(t), Horner over the (canonical) coefficients
+  T pt = FO::zero();
+  for (uint32_t d = gp_len; d-- > 0;) {
+    const T c = FO::load(gp + (size_t)d * ES);
+    bad |= !FO::is_canonical(c);
+    pt = FO::add(FO::mul(tm, pt), c);
+  }
+
+  // gadget-output combination
+  T vn = FO::zero(), vd = one, extra = FO::zero();
+  if (cfg.kind == KIND_COUNT) {
+    const T al = ld_tw<FO>(cfg, 1);
+    T pa = FO::zero();
+    for (uint32_t d = gp_len; d-- > 0;) pa = FO::add(FO::mul(al, pa), FO::load(gp + (size_t)d * ES));
+    extra = FO::sub(pa, x0);
+  } else {  // KIND_SUM
+    const T rm = FO::to_mont(FO::load(jr.at(r)));
+    const T rc = mont_pow<FO>(rm, calls);  // r^calls
+    const T calls_m = FO::to_mont(FO::from_u32(calls));
+    for (uint32_t i = 0; i < m; ++i) {
+      T f = FO::load(gp + (size_t)i * ES);
+      if (i + m < gp_len) f = FO::add(f, FO::load(gp + (size_t)(i + m) * ES));
+      const T y = FO::mul(rm, ld_tw<FO>(cfg, i));
+      const T e = FO::sub(y, one);
+      if (FO::is_zero(e)) {  // y == 1: G = calls
+        extra = FO::add(extra, FO::mul(calls_m, f));
+        continue;
+      }
+      const T yc = FO::mul(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)i * calls) % m)));
+      const T b = FO::mul(FO::mul(y, f), FO::sub(yc, one));
+      vn = FO::add(FO::mul(vn, e), FO::mul(b, vd));
+      vd = FO::mul(vd, e);
+    }
+  }
+  // one inversion for both denominators
+  const T inv = inv_mont<FO>(FO::mul(dw, vd));
+  const T dinv = FO::mul(inv, vd), vinv = FO::mul(inv, dw);
+  const T w0 = FO::mul(cm, FO::mul(nw0, dinv));
+  const T v = FO::add(FO::mul(vn, vinv), extra);
+
+  uint8_t* outp = out_prep.at(r);
+  FO::store(outp, v);
+  FO::store(outp + ES, w0);
+  if (arity > 1) FO::store(outp + 2 * ES, FO::mul(cm, FO::mul(nw1, dinv)));
+  FO::store(outp + (size_t)(1 + arity) * ES, pt);
+  if (cfg.jr_len > 0) {
+    const uint8_t* pp = part.at(r);
+    uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
+    st64(dst, ld64(pp));
+    st64(dst + 8, ld64(pp + 8));
+  }
+  if (bad) status[r] = ST_INVALID_MESSAGE;
+  else if (root) status[r] = ST_VDAF_PREP_ERROR;
+}
+
+// ------------------------------------------------------------------------------------------------
 // FLP query, ParallelSum types, first half, one WAVE per report (m <= 128, chunk <= 128): the same
 // weights as k_flp_query's split mode, computed in registers with cross-lane shuffles instead of
 // LDS tables and block barriers (no LDS at all, so occupancy is set by VGPRs alone):
@@ -1434,7 +1563,31 @@ __global__ void __launch_bounds__(256) k_decide(Cfg cfg, uint32_t n, CRows leade
   const size_t ES = FO::ES;
   const uint32_t npairs = cfg.kind == KIND_SUM ? 1u : cfg.arity / 2u;
   bool mine = false;
-  for (uint32_t q = 0; q < nr; ++q) {
+  if (npairs == 1u) {  // Count / Sum: one gadget evaluation, each lane decides its own report
+    const uint32_t rq = r0 + lane;
+    if (lane < nr && status[rq] == ST_OK) {
+      const uint8_t* a = leader_prep.at(rq);
+      const uint8_t* b = helper_prep.at(rq);
+      const T x0 = FO::load(a + ES), y0 = FO::load(b + ES);
+      bool bad = !FO::is_canonical(x0) || !FO::is_canonical(y0);
+      const T w0 = FO::add(x0, y0);
+      T g;
+      if (cfg.kind == KIND_SUM) {
+        g = FO::sub(FO::mul(FO::to_mont(w0), w0), w0);
+      } else {
+        const T x1 = FO::load(a + 2 * ES), y1 = FO::load(b + 2 * ES);
+        bad |= !FO::is_canonical(x1) || !FO::is_canonical(y1);
+        g = FO::mul(FO::to_mont(w0), FO::add(x1, y1));
+      }
+      const T va = FO::load(a), vb = FO::load(b);
+      const T pa = FO::load(a + (size_t)(1u + cfg.arity) * ES);
+      const T pb = FO::load(b + (size_t)(1u + cfg.arity) * ES);
+      bad |= !FO::is_canonical(va) || !FO::is_canonical(vb) || !FO::is_canonical(pa) ||
+             !FO::is_canonical(pb);
+      mine = !bad && FO::is_zero(FO::add(va, vb)) && FO::eq(g, FO::add(pa, pb));
+    }
+  }
+  for (uint32_t q = 0; q < (npairs == 1u ? 0u : nr); ++q) {
     const uint32_t rq = r0 + q;
     if (__builtin_amdgcn_readfirstlane(status[rq]) != ST_OK) continue;  // wave-uniform
     const uint8_t* a = leader_prep.at(rq);
@@ -1646,38 +1799,59 @@ __global__ void __launch_bounds__(256) k_accum_merge(Cfg cfg, uint32_t nchunks,
                                                      const uint32_t* part_counts, uint8_t* agg,
                                                      unsigned long long* counts) {
   using T = typename FO::T;
-  __shared__ T sums[256];
+  __shared__ T part[256];
+  __shared__ T tot[256];
   const uint32_t bpe =
       (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_SUM || cfg.kind == KIND_FPVEC) ? cfg.bits : 1u;
   const uint32_t opb = 256 / bpe;  // output elements per block
+  const uint32_t o0 = blockIdx.x * opb;
+  const uint32_t nout = min(opb, cfg.out_len - o0);
+  // ne measurement elements in this block; when they leave threads idle (Count, Sum: one output)
+  // L threads share an element, each summing every L-th chunk of a run, then an LDS fold
+  const uint32_t ne = nout * bpe;
+  const uint32_t L = 256 / ne;
   const uint32_t tid = threadIdx.x;
-  const uint32_t o = blockIdx.x * opb + tid / bpe, b = tid % bpe;
-  const bool act = (tid < opb * bpe) && o < cfg.out_len;
+  const uint32_t el = tid % ne, g = tid / ne;
+  const bool act = g < L;
+  const uint32_t o = o0 + el / bpe, b = el % bpe;
   const uint32_t e = o * bpe + b;
   uint32_t c = 0;
   while (c < nchunks) {
     const uint32_t slot = chunk_slot[c];
-    uint32_t c1 = c;
-    while (c1 < nchunks && chunk_slot[c1] == slot) ++c1;
+    // end of this slot's run: a slot's chunks are contiguous, so "== slot" holds exactly on
+    // [c, c1) of [c, nchunks) and a binary search finds c1
+    uint32_t lo = c + 1, hi = nchunks;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (chunk_slot[mid] == slot) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint32_t c1 = lo;
     T acc = FO::zero();
     if (act) {
 #pragma unroll 4
-      for (uint32_t q = c; q < c1; ++q)
+      for (uint32_t q = c + g; q < c1; q += L)
         acc = FO::add(acc, FO::load(partials + ((size_t)q * cfg.meas_len + e) * FO::ES));
     }
-    sums[tid] = acc;
+    part[tid] = acc;
     __syncthreads();
-    if (act && b == 0) {
+    if (g == 0) {
+      for (uint32_t gg = 1; gg < L; ++gg) acc = FO::add(acc, part[gg * ne + el]);
+      tot[el] = acc;
+    }
+    __syncthreads();
+    if (g == 0 && b == 0) {
       T t = FO::zero();
-      for (int k = (int)bpe - 1; k >= 0; --k) t = FO::add(FO::dbl(t), sums[tid + k]);
+      for (int k = (int)bpe - 1; k >= 0; --k) t = FO::add(FO::dbl(t), tot[el + k]);
       uint8_t* dst = agg + ((size_t)slot * cfg.out_len + o) * FO::ES;
       FO::store(dst, FO::add(FO::load(dst), t));
     }
     __syncthreads();
     c = c1;
   }
-  if (blockIdx.x == 0 && tid == 0) {
-    for (uint32_t q = 0; q < nchunks; ++q) counts[chunk_slot[q]] += part_counts[q];
+  if (blockIdx.x == 0) {  // report counts: integer adds, order-free
+    for (uint32_t q = tid; q < nchunks; q += blockDim.x)
+      if (part_counts[q]) atomicAdd(&counts[chunk_slot[q]], (unsigned long long)part_counts[q]);
   }
 }
 

@@ -8,6 +8,9 @@
 //   st16nt   : st16 with non-temporal stores
 //   ld16     : + 11 x 16-B loads of the lane's own row, absorbed (per-lane row-strided loads)
 //   lds      : + 10 ds_write_b128 + 10 ds_read_b128 of a 160-B LDS row (no global traffic)
+//   st16c    : + 10 x 16-B stores, COALESCED: the wave's 64 lanes write 1 KB contiguous per store
+//              (a 64-report tile, element-major), instead of one row per lane
+//   ld16c    : + 11 x 16-B loads, coalesced the same way
 //   *_stg    : the same with odd blocks starting half a permutation late (breaks the lockstep of
 //              the waves that share a SIMD, so their memory phases do not coincide)
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/mb_keccak_occ tools/mb_keccak_occ.hip
@@ -38,6 +41,16 @@ __global__ void __launch_bounds__(256) k_var(uint32_t* out, uint32_t seed, uint8
   for (int i = 0; i < 25; ++i) s[i] = (uint64_t)(seed + threadIdx.x) * (i + 1);
   if (STG && (blockIdx.x & 1)) keccak_p<12>(s);
   for (int it = 0; it < PERMS; ++it) {
+    if constexpr (V == 7) {  // ld16c
+      const ulonglong2* src = reinterpret_cast<const ulonglong2*>(
+          rows + (gid >> 6) * 64 * ROW + ((size_t)it * 10 * 64 + (gid & 63)) * 16);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        const ulonglong2 v = src[k * 64];
+        s[2 * k] ^= v.x;
+        s[2 * k + 1] ^= v.y;
+      }
+    }
     if constexpr (V == 4) {  // ld16
       const ulonglong2* src = reinterpret_cast<const ulonglong2*>(row + (size_t)it * 168);
 #pragma unroll
@@ -56,6 +69,11 @@ __global__ void __launch_bounds__(256) k_var(uint32_t* out, uint32_t seed, uint8
       ulonglong2* d = reinterpret_cast<ulonglong2*>(row + (size_t)(it & ~1) * 168);
 #pragma unroll
       for (int k = 0; k < 10; ++k) d[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
+    } else if constexpr (V == 6) {
+      ulonglong2* d = reinterpret_cast<ulonglong2*>(
+          rows + (gid >> 6) * 64 * ROW + ((size_t)(it & ~1) * 10 * 64 + (gid & 63)) * 16);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) d[k * 64] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
     } else if constexpr (V == 3) {
       ulonglong2* d = reinterpret_cast<ulonglong2*>(row + (size_t)(it & ~1) * 168);
 #pragma unroll
@@ -116,10 +134,9 @@ int main() {
   CK(hipMalloc(&d, lanes * 4));
   CK(hipMalloc(&rows, lanes * ROW));
   CK(hipMemset(rows, 0, lanes * ROW));
-  const char* names[8] = {"reg", "st16", "ld16", "lds", "reg_stg", "st16_stg", "ld16_stg", "lds_stg"};
-  kfn ks[8] = {k_var<0>, k_var<2>, k_var<4>, k_var<5>,
-               k_var<0, true>, k_var<2, true>, k_var<4, true>, k_var<5, true>};
-  for (int v = 0; v < 8; ++v)
+  const char* names[6] = {"reg", "st16", "st16c", "ld16", "ld16c", "lds"};
+  kfn ks[6] = {k_var<0>, k_var<2>, k_var<6>, k_var<4>, k_var<7>, k_var<5>};
+  for (int v = 0; v < 6; ++v)
     for (int k = 2; k <= 4; ++k) run(names[v], ks[v], k, d, rows, rounds);
   CK(hipFree(d));
   CK(hipFree(rows));
