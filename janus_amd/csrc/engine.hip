@@ -722,8 +722,11 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
   if (psum) {
     dims.cols = g.chunk;
     if (g.chunk <= c->wires_slots) {
+      // row groups: up to the slot budget, but at least ~4 rows per thread, so that short
+      // reports (Histogram256: 16 calls) do not spend a block of mostly idle threads per report
+      // (A/B, profiles/r02/ab_hist_slots*.log: H 16 -> 4 took k_flp_wires 18.0 -> 6.1 ms/step)
       dims.H = c->wires_slots / g.chunk;
-      if (dims.H > g.calls) dims.H = g.calls;
+      dims.H = std::min(dims.H, std::max(1u, g.calls / 4));
       nthr = ((dims.H * g.chunk + 63) / 64) * 64;
     } else {
       dims.H = 1;

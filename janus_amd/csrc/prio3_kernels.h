@@ -1587,7 +1587,49 @@ __global__ void __launch_bounds__(256) k_decide(Cfg cfg, uint32_t n, CRows leade
       mine = !bad && FO::is_zero(FO::add(va, vb)) && FO::eq(g, FO::add(pa, pb));
     }
   }
-  for (uint32_t q = 0; q < (npairs == 1u ? 0u : nr); ++q) {
+  // npairs <= 32 (Histogram256: 16): several reports per pass, a power-of-two lane group each,
+  // reduced with in-group xor shuffles
+  uint32_t G = 1u;
+  while (G < npairs) G <<= 1;
+  if (npairs > 1u && G < 64u) {
+    const uint32_t rpi = 64u / G, sub = lane / G, lj = lane % G;
+    for (uint32_t q0 = 0; q0 < nr; q0 += rpi) {
+      const uint32_t rq = r0 + q0 + sub;
+      const bool on = q0 + sub < nr && status[rq] == ST_OK;
+      bool bad = false;
+      T g = FO::zero();
+      const uint8_t* a = leader_prep.at(on ? rq : r0);
+      const uint8_t* b = helper_prep.at(on ? rq : r0);
+      if (on && lj < npairs) {
+        const uint8_t* pa = a + (size_t)(1u + 2u * lj) * ES;
+        const uint8_t* pb = b + (size_t)(1u + 2u * lj) * ES;
+        const T x0 = FO::load(pa), x1 = FO::load(pa + ES);
+        const T y0 = FO::load(pb), y1 = FO::load(pb + ES);
+        bad = !FO::is_canonical(x0) || !FO::is_canonical(x1) || !FO::is_canonical(y0) ||
+              !FO::is_canonical(y1);
+        g = FO::mul(FO::to_mont(FO::add(x0, y0)), FO::add(x1, y1));
+      }
+      uint32_t badw = bad ? 1u : 0u;
+      for (uint32_t off = G >> 1; off >= 1u; off >>= 1) {
+        g = FO::add(g, shfl_xor_T<FO>(g, (int)off));
+        badw |= (uint32_t)__shfl_xor((int)badw, (int)off, 64);
+      }
+      bool ok = false;
+      if (on) {
+        const T va = FO::load(a), vb = FO::load(b);
+        const T pa = FO::load(a + (size_t)(1u + cfg.arity) * ES);
+        const T pb = FO::load(b + (size_t)(1u + cfg.arity) * ES);
+        const bool bad2 = !FO::is_canonical(va) || !FO::is_canonical(vb) ||
+                          !FO::is_canonical(pa) || !FO::is_canonical(pb);
+        ok = !badw && !bad2 && FO::is_zero(FO::add(va, vb)) && FO::eq(g, FO::add(pa, pb));
+      }
+      // report q0 + s's decision sits in every lane of group s: lane q0 + s takes it
+      const uint32_t src = lane >= q0 && lane < q0 + rpi ? (lane - q0) * G : 0u;
+      const bool got = __shfl((int)ok, (int)src, 64) != 0;
+      if (lane >= q0 && lane < q0 + rpi) mine = got;
+    }
+  }
+  for (uint32_t q = 0; q < (npairs == 1u || G < 64u ? 0u : nr); ++q) {
     const uint32_t rq = r0 + q;
     if (__builtin_amdgcn_readfirstlane(status[rq]) != ST_OK) continue;  // wave-uniform
     const uint8_t* a = leader_prep.at(rq);
