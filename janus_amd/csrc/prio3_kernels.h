@@ -938,8 +938,11 @@ DEVI typename FO::T inv_mont(const typename FO::T& x) {
   else return mont_pow<FO>(x, Field64Ops::P - 2ull);
 }
 
+#ifndef FLPQ_WAVES
+#define FLPQ_WAVES
+#endif
 template <class FO>
-__global__ void __launch_bounds__(256) k_flp_query_lane(Cfg cfg, uint32_t n, CRows meas,
+__global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint32_t n, CRows meas,
                                                         CRows proof, CRows tq, CRows jr,
                                                         CRows part, Rows out_prep,
                                                         uint8_t* status) {
