@@ -972,61 +972,97 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
     x0 = FO::load(xr);
     bad |= !FO::is_canonical(x0);
   }
-  for (uint32_t k = 0; k <= calls; ++k) {
+  // k-th term of the wire fraction (k >= 1; k = 0 is peeled: a = the proof seed)
+  auto wire_step = [&](uint32_t k) {
     const T ak = ld_tw<FO>(cfg, k);  // alpha^k, Montgomery
     const T d = FO::sub(tm, ak);
-    T a0, a1;
-    if (k == 0) {
-      a0 = s0;
-      a1 = s1;
-    } else {
-      T x = x0;
-      if (cfg.kind != KIND_COUNT) {
-        x = FO::load(xr + (size_t)(k - 1) * ES);
-        bad |= !FO::is_canonical(x);
-      }
-      a0 = FO::mul(ak, x);
-      a1 = a0;
+    T x = x0;
+    if (cfg.kind != KIND_COUNT) {
+      x = FO::load(xr + (size_t)(k - 1) * ES);
+      bad |= !FO::is_canonical(x);
     }
-    nw0 = FO::add(FO::mul(nw0, d), FO::mul(a0, dw));
-    if (arity > 1) nw1 = FO::add(FO::mul(nw1, d), FO::mul(a1, dw));
+    const T a = FO::mul(ak, x);
+    nw0 = FO::add(FO::mul(nw0, d), FO::mul(a, dw));
+    if (arity > 1) nw1 = FO::add(FO::mul(nw1, d), FO::mul(a, dw));
     dw = FO::mul(dw, d);
-  }
+  };
 
-  // p(t), Horner over the (canonical) coefficients
   T pt = FO::zero();
-  for (uint32_t d = gp_len; d-- > 0;) {
-    const T c = FO::load(gp + (size_t)d * ES);
-    bad |= !FO::is_canonical(c);
-    pt = FO::add(FO::mul(tm, pt), c);
-  }
-
-  // gadget-output combination
   T vn = FO::zero(), vd = one, extra = FO::zero();
   if (cfg.kind == KIND_COUNT) {
+    for (uint32_t k = calls; k >= 1; --k) wire_step(k);
+    for (uint32_t d = gp_len; d-- > 0;) {  // p(t) by Horner
+      const T c = FO::load(gp + (size_t)d * ES);
+      bad |= !FO::is_canonical(c);
+      pt = FO::add(FO::mul(tm, pt), c);
+    }
     const T al = ld_tw<FO>(cfg, 1);
     T pa = FO::zero();
     for (uint32_t d = gp_len; d-- > 0;) pa = FO::add(FO::mul(al, pa), FO::load(gp + (size_t)d * ES));
     extra = FO::sub(pa, x0);
-  } else {  // KIND_SUM
+  } else {  // KIND_SUM: one pass over i = m-1 .. 0 carrying three independent chains
+    // (Horner on p(t) = sum_i (c_i + c_(i+m) t^m) t^i, the v fraction over G(r alpha^i), and for
+    // i <= calls the wire fraction), so the Montgomery carry chains of one fill the other's
+    // hazard slots; y_i = r alpha^i == 1 needs r^m == 1, handled outside the loop.
     const T rm = FO::to_mont(FO::load(jr.at(r)));
     const T rc = mont_pow<FO>(rm, calls);  // r^calls
-    const T calls_m = FO::to_mont(FO::from_u32(calls));
-    for (uint32_t i = 0; i < m; ++i) {
-      T f = FO::load(gp + (size_t)i * ES);
-      if (i + m < gp_len) f = FO::add(f, FO::load(gp + (size_t)(i + m) * ES));
+    T rmm = rm;
+    for (uint32_t q = 0; q < cfg.logm; ++q) rmm = FO::mul(rmm, rmm);
+    const bool r_root = FO::eq(rmm, one);
+    auto coeffs = [&](uint32_t i, T& ci, T& ch) {
+      ci = FO::load(gp + (size_t)i * ES);
+      ch = i + m < gp_len ? FO::load(gp + (size_t)(i + m) * ES) : FO::zero();
+      bad |= !FO::is_canonical(ci) || !FO::is_canonical(ch);
+    };
+    auto v_step = [&](uint32_t i, const T& f) {
       const T y = FO::mul(rm, ld_tw<FO>(cfg, i));
       const T e = FO::sub(y, one);
-      if (FO::is_zero(e)) {  // y == 1: G = calls
-        extra = FO::add(extra, FO::mul(calls_m, f));
-        continue;
-      }
       const T yc = FO::mul(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)i * calls) % m)));
       const T b = FO::mul(FO::mul(y, f), FO::sub(yc, one));
       vn = FO::add(FO::mul(vn, e), FO::mul(b, vd));
       vd = FO::mul(vd, e);
+    };
+    if (!r_root) {
+      for (uint32_t i = m - 1; i > calls; --i) {
+        T ci, ch;
+        coeffs(i, ci, ch);
+        pt = FO::add(FO::mul(tm, pt), FO::add(ci, FO::mul(tmm, ch)));
+        v_step(i, FO::add(ci, ch));
+      }
+      for (uint32_t i = calls; i >= 1; --i) {
+        T ci, ch;
+        coeffs(i, ci, ch);
+        pt = FO::add(FO::mul(tm, pt), FO::add(ci, FO::mul(tmm, ch)));
+        v_step(i, FO::add(ci, ch));
+        wire_step(i);
+      }
+      T ci, ch;
+      coeffs(0, ci, ch);
+      pt = FO::add(FO::mul(tm, pt), FO::add(ci, FO::mul(tmm, ch)));
+      v_step(0, FO::add(ci, ch));
+    } else {  // r^m == 1 (probability ~m / p): some y_i == 1, where G = calls
+      for (uint32_t k = calls; k >= 1; --k) wire_step(k);
+      const T calls_m = FO::to_mont(FO::from_u32(calls));
+      for (uint32_t i = m; i-- > 0;) {
+        T ci, ch;
+        coeffs(i, ci, ch);
+        pt = FO::add(FO::mul(tm, pt), FO::add(ci, FO::mul(tmm, ch)));
+        const T f = FO::add(ci, ch);
+        if (FO::is_zero(FO::sub(FO::mul(rm, ld_tw<FO>(cfg, i)), one)))
+          extra = FO::add(extra, FO::mul(calls_m, f));
+        else
+          v_step(i, f);
+      }
     }
   }
+  // the k = 0 wire term: a = the proof seed
+  {
+    const T d = FO::sub(tm, one);
+    nw0 = FO::add(FO::mul(nw0, d), FO::mul(s0, dw));
+    if (arity > 1) nw1 = FO::add(FO::mul(nw1, d), FO::mul(s1, dw));
+    dw = FO::mul(dw, d);
+  }
+
   // one inversion for both denominators
   const T inv = inv_mont<FO>(FO::mul(dw, vd));
   const T dinv = FO::mul(inv, vd), vinv = FO::mul(inv, dw);

@@ -141,3 +141,53 @@ def test_speculative_matches_direct_and_plaintext(name):
         (la, lc), (ha, hc) = out["spec"][2][q], out["spec"][3][q]
         assert lc == hc == int(sel.sum())
         assert vs.unshard([la, ha]) == _plain(name, meas, sel)
+
+
+@pytest.mark.parametrize("kind,bits,label", [(0, 0, "count"), (1, 32, "sum32"), (1, 8, "sum8")])
+def test_small_types_multichunk_slots_bytes_vs_c_restatement(kind, bits, label):
+    """Count / Sum at a size with several 2,048-report accumulation chunks per batch slot: the
+    lane-per-report FLP query and decide (k_flp_query_lane, k_decide's lane path) and the merge
+    that splits each slot's chunk run over otherwise idle threads (k_accum_merge, runs found by
+    binary search, counts by atomics).  10,000 reports over 3 randomly interleaved slots, a few
+    tampered; per-slot aggregate bytes and counts of both aggregators == the C restatement."""
+    from janus_amd.prio3 import Prio3Gpu
+    from oracle import prio3 as O
+    from oracle.ref import Prio3Ref
+    n = 10000
+    cfg = f"merge-{label}".encode()
+    vk = O.synth_verify_key(cfg)
+    ref = Prio3Ref(kind, vk, bits, 0, 0)
+    g = ref.gen(cfg, 0, n, threads=16)
+    es = 8 if kind == 0 else 16
+    p = O.Field64.MODULUS if kind == 0 else O.Field128.MODULUS
+    lin = g["leader_in"].copy()
+    bad = [3, 2047, 2048, 6001, 9999]
+    for r in bad:  # + 2: a bit becomes 2 or 3 (+ 1 could turn Count's 0 into a valid 1)
+        x = (int.from_bytes(lin[r, :es].tobytes(), "little") + 2) % p
+        lin[r, :es] = np.frombuffer(x.to_bytes(es, "little"), np.uint8)
+    slots = np.random.default_rng(5).integers(0, 3, n).astype(np.uint32)
+    v = Prio3Gpu(kind, vk, bits=bits)
+    pub = g["public"] if g["public"].shape[1] else None
+    ls, hs = v.new_state(0, n), v.new_state(1, n)
+    lp, lst = v.prepare_init(ls, g["nonces"], pub, lin)
+    hagg, lagg = v.new_aggregate(3), v.new_aggregate(3)
+    msgs, hst = v.helper_init(hs, g["nonces"], pub, g["helper_in"], lp, agg=hagg,
+                              batch_slots=slots)
+    # the helper's Reject reaches the leader in the AggregationJobResp (Count has no prep message
+    # to disagree on): the leader driver carries it into prepare_next's status
+    lst = np.where(hst != 0, hst, lst).astype(np.uint8)
+    _, lst = v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg, batch_slots=slots)
+    ok = np.ones(n, bool)
+    ok[bad] = False
+    assert (hst[bad] == 5).all() and (hst[ok] == 0).all() and (lst == hst).all()
+    for q in range(3):
+        sel = np.nonzero(slots == q)[0]
+        res = ref.prepare_batch(np.ascontiguousarray(g["nonces"][sel]),
+                                np.ascontiguousarray(g["public"][sel]),
+                                np.ascontiguousarray(lin[sel]),
+                                np.ascontiguousarray(g["helper_in"][sel]), threads=16,
+                                outputs=False)
+        (la, lc), (ha, hc) = lagg.read(q), hagg.read(q)
+        assert lc == hc == res["count"] == int(ok[sel].sum())
+        assert la == res["agg_l"].tobytes(), f"leader slot {q}"
+        assert ha == res["agg_h"].tobytes(), f"helper slot {q}"
