@@ -121,6 +121,12 @@ def reduce_program():
 
 REDUCE = reduce_program()
 
+# Temporaries of the reduction live in registers that are dead by then: g0..g5 once chain A has
+# folded them into T (g6 holds T7), h1..h5 once chain B has.  check() verifies the aliasing by
+# simulating with shared storage.
+ALIAS = {"m0": "g0", "m1": "g1", "a0": "g2", "a1": "g3", "a2": "g4", "b0": "g5", "b1": "h1",
+         "b2": "h2", "w0": "h3", "w1": "h4", "w2": "h5"}
+
 
 # ---------------------------------------------------------------------------------------------
 # Simulator (one lane)
@@ -183,7 +189,8 @@ def check(trials=20000):
             st[f"l{c}"] = st[f"L{c}"] & M32
             st[f"g{c}"] = st[f"L{c}"] >> 32
         st["v4"] = 0
-        simulate(REDUCE, st)
+        simulate([tuple(ALIAS.get(x, x) if isinstance(x, str) else x for x in ins)
+                  for ins in REDUCE], st)
         r = sum(st[f"r{i}"] << (32 * i) for i in range(4))
         assert r == mont_ref(a, b), (hex(a), hex(b), hex(r), hex(mont_ref(a, b)))
     # hazard rule inside one stream: a carry is never read by the very next instruction of the
@@ -265,12 +272,11 @@ def emit():
     ops, cons, idx = [], [], {}
     regs = (["l%d" % c for c in range(7)] + ["g%d" % c for c in range(7)] +
             ["h%d" % c for c in range(1, 6)] + ["v4"])
-    tmps = ["m0", "m1", "a0", "a1", "a2", "b0", "b1", "b2", "w0", "w1", "w2"]
+    tmps = []  # every temporary lives in a register the normalisation has freed (ALIAS)
     for s in range(NS):
         w(f"  uint32_t l{s}[7], g{s}[7], v4_{s} = 0u;")
         w(f"  for (int c = 0; c < 7; ++c) {{ l{s}[c] = (uint32_t)L{s}[c]; "
           f"g{s}[c] = (uint32_t)(L{s}[c] >> 32); }}")
-        w(f"  uint32_t t{s}[{len(tmps)}];")
         w(f"  uint64_t k{s}, kk{s};")
     for s in range(NS):
         for r in regs:
@@ -280,8 +286,8 @@ def emit():
                 opnd(f"{r}_{s}", '"+v"', f"h{s}[{int(r[1:]) - 1}]")
             else:
                 opnd(f"{r}_{s}", '"+v"', f"v4_{s}")
-        for i, t in enumerate(tmps):
-            opnd(f"{t}_{s}", '"=&v"', f"t{s}[{i}]")
+        for t, reg in ALIAS.items():
+            idx[f"{t}_{s}"] = idx[f"{reg}_{s}"]
         for i in range(4):
             opnd(f"r{i}_{s}", '"=&v"', f"r{s}.w[{i}]")
         opnd(f"k_{s}", '"=&s"', f"k{s}")
