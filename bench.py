@@ -217,6 +217,10 @@ def main():
                     help="XofShake128 (prio 0.15.1 / VDAF-07: the reference's XOF, the metric) or "
                          "XofTurboShake128 (VDAF-08+, the north star's Keccak-p[1600,12]; the C "
                          "restatement is SHAKE128-only, so its gates use the Python oracle)")
+    ap.add_argument("--merge", default="rccl", choices=["rccl", "gloo"],
+                    help="N > 1: per-step RCCL all-gather + mod-p merge (the product path), or "
+                         "'gloo' = a rehearsal of the multi-rank bench on fewer GPUs than ranks "
+                         "(ranks share GPUs, aggregates merged once over gloo at the end)")
     ap.add_argument("--workers", type=int, default=1,
                     help="concurrent aggregation-job workers per GPU, one engine context (HIP "
                          "stream) and one contiguous slice of the batch each (Janus "
@@ -230,8 +234,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # the device of this rank (gloo rehearsal: ranks may share GPUs)
+    gpu = local_rank % max(1, torch.cuda.device_count()) if args.merge == "gloo" else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         # Host-side coordination only (barriers, max-over-ranks timing, the RCCL unique id):
@@ -258,7 +264,7 @@ def main():
     W = max(1, args.workers)
     turbo = args.xof == "turboshake128"
     xof_id = XOF_TURBOSHAKE128 if turbo else XOF_SHAKE128
-    vdafs = [Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=local_rank,
+    vdafs = [Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk, device=gpu,
                       xof=xof_id) for _ in range(W)]
     vdaf = vdafs[0]
     s = vdaf.sizes
@@ -305,10 +311,11 @@ def main():
     torch.cuda.synchronize()
 
     comm = None
-    if world > 1:
+    rccl = world > 1 and args.merge == "rccl"
+    if rccl:
         uid = [Comm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        comm = Comm(uid[0], world, rank, local_rank)
+        comm = Comm(uid[0], world, rank, gpu)
     L = lib()
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -327,10 +334,10 @@ def main():
         # --overlap: the helper gets its own context (HIP stream), so its prepare_init runs
         # concurrently with the leader's, like two aggregator processes sharing the GPU
         wk.hv = (Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk,
-                          device=local_rank, xof=xof_id) if args.overlap else wk.v)
+                          device=gpu, xof=xof_id) if args.overlap else wk.v)
         wk.ls, wk.hs = wk.v.new_state(0, wk.n), wk.hv.new_state(1, wk.n)
         wk.lagg, wk.hagg = wk.v.new_aggregate(1), wk.hv.new_aggregate(1)
-        wk.lpart, wk.hpart = ((wk.v.new_aggregate(1), wk.hv.new_aggregate(1)) if world > 1
+        wk.lpart, wk.hpart = ((wk.v.new_aggregate(1), wk.hv.new_aggregate(1)) if rccl
                               else (wk.lagg, wk.hagg))
         sl = slice(lo, hi)
         wk.p = dict(nonces=P(d_nonces[sl]), pub=P(d_pub[sl]) if d_pub is not None else None,
@@ -515,6 +522,20 @@ def main():
 
     la, lc = total("lagg")
     ha, hc = total("hagg")
+    if dist is not None and not rccl:  # gloo rehearsal: merge the ranks' aggregates on the host
+        for which in ("l", "h"):
+            mine = (la, lc) if which == "l" else (ha, hc)
+            allv = [None] * world
+            dist.all_gather_object(allv, mine)
+            acc = [0] * (len(mine[0]) // s.field_size)
+            for b, _ in allv:
+                acc = [(x + y) % vdaf.modulus for x, y in zip(acc, vdaf.decode_field_vec(b))]
+            merged = (b"".join(int(x).to_bytes(s.field_size, "little") for x in acc),
+                      sum(c for _, c in allv))
+            if which == "l":
+                la, lc = merged
+            else:
+                ha, hc = merged
     exp_count = total_steps * B * world
     assert lc == exp_count and hc == exp_count, (lc, hc, exp_count)
     meas = syn["meas"]
@@ -782,7 +803,8 @@ def main():
         "config": {"workload": label, "xof": "XofTurboShake128" if turbo else "XofShake128",
                    "reports_per_gpu_per_step": B, "job_workers_per_gpu": W,
                    "parallelism": f"report-sharded x{world}, {W} job stream(s)/GPU, "
-                                  f"RCCL all-gather merge"},
+                                  + ("RCCL all-gather merge" if args.merge == "rccl" else
+                                     "gloo rehearsal (ranks share GPUs, host merge)")},
         "roofline": roof,
         "cpu_baseline": cpu,
         "hpke_open": hpke_rep,
