@@ -60,8 +60,8 @@ enum prio3gpu_kind {
   /* Prio3FixedPoint{16,32,64}BitBoundedL2VecSum { length } (core/src/task.rs:24-59,
    * aggregator.rs:839-861): bits = 16/32/64 (FixedI16<U15>/FixedI32<U31>/FixedI64<U63>),
    * length = entries; chunk_length is ignored (prio picks both gadgets' chunk lengths with
-   * optimal_chunk_length).  Field128, algorithm ID 0xFFFF0000.  Measurements for prio3gpu_shard
-   * are not supported for this kind (clients shard on the CPU). */
+   * optimal_chunk_length).  Field128, algorithm ID 0xFFFF0000.  prio3gpu_shard takes the raw
+   * two's-complement entries (see there). */
   PRIO3GPU_FPVEC = 4
 };
 
