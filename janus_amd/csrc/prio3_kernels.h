@@ -21,6 +21,7 @@
 #include "field.h"
 #include "keccak.h"
 #include "wide.h"
+#include "mont3.h"
 
 namespace p3g {
 
@@ -932,6 +933,29 @@ __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims 
 // 64 threads with a barrier per stage.  A zero t - alpha^k means t^m == 1: VdafPrepError (prio's
 // "root of unity" rejection); the values computed then are discarded.
 // ------------------------------------------------------------------------------------------------
+// three independent Montgomery products: mont_mul3 for Field128, plain products for Field64
+template <class FO>
+DEVI void mul3(const typename FO::T& a0, const typename FO::T& b0, const typename FO::T& a1,
+               const typename FO::T& b1, const typename FO::T& a2, const typename FO::T& b2,
+               typename FO::T& r0, typename FO::T& r1, typename FO::T& r2) {
+  if constexpr (FO::ES == 16) {
+    F128 t0, t1, t2;
+    mont_mul3(a0, b0, a1, b1, a2, b2, t0, t1, t2);
+    r0 = t0;
+    r1 = t1;
+    r2 = t2;
+  } else {
+    const typename FO::T t0 = FO::mul(a0, b0), t1 = FO::mul(a1, b1), t2 = FO::mul(a2, b2);
+    r0 = t0;
+    r1 = t1;
+    r2 = t2;
+  }
+}
+
+#ifndef FLPQ_MUL3
+#define FLPQ_MUL3 1
+#endif
+
 template <class FO>
 DEVI typename FO::T inv_mont(const typename FO::T& x) {
   if constexpr (FO::ES == 16) return inv_mont128(x);
@@ -1022,7 +1046,58 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
       vn = FO::add(FO::mul(vn, e), FO::mul(b, vd));
       vd = FO::mul(vd, e);
     };
-    if (!r_root) {
+    if (!r_root && FLPQ_MUL3) {
+      // the same three chains, every iteration's products issued as hazard-free triples
+      // (mont_mul3, Field128).  b_i * vd is refactored as (y f) * ((yc - 1) vd) so the
+      // 12 (13) products of a wire iteration form 4 triples (+1 single); when calls == m / 2
+      // (Sum with power-of-two bits) yc = r^calls alpha^(i calls) = +-r^calls needs no product.
+      const bool half = 2u * calls == m;
+      const T ycm_even = FO::sub(rc, one), ycm_odd = FO::sub(FO::sub(FO::zero(), rc), one);
+      for (uint32_t i = m - 1;; --i) {
+        const bool wire = i >= 1 && i <= calls;
+        T ci, ch;
+        coeffs(i, ci, ch);
+        T x = FO::zero();
+        if (wire) {
+          x = FO::load(xr + (size_t)(i - 1) * ES);
+          bad |= !FO::is_canonical(x);
+        }
+        const T f = FO::add(ci, ch);
+        const T twi = ld_tw<FO>(cfg, i);
+        const T d = FO::sub(tm, twi);
+        T q, y, u, a, P, dwn, g, yf, vde, vne, adw, nwd, yfg;
+        // triple 1: q = t^m c_(i+m), y = r alpha^i, u = (half ? g : yc)
+        if (half) {
+          const T ycm = (i & 1u) ? ycm_odd : ycm_even;
+          mul3<FO>(tmm, ch, rm, twi, ycm, vd, q, y, g);
+        } else {
+          mul3<FO>(tmm, ch, rm, twi, rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)i * calls) % m)), q,
+                   y, u);
+        }
+        // triple 2: P = t pt, and for wire iterations a = alpha^i x, dw d
+        if (wire) {
+          mul3<FO>(tm, pt, twi, x, dw, d, P, a, dwn);
+        } else {
+          P = FO::mul(tm, pt);
+        }
+        if (!half) g = FO::mul(FO::sub(u, one), vd);
+        const T e = FO::sub(y, one);
+        // triple 3: y f, vd e, vn e
+        mul3<FO>(y, f, vd, e, vn, e, yf, vde, vne);
+        if (wire) {
+          // triple 4: a dw, nw0 d, (y f) g
+          mul3<FO>(a, dw, nw0, d, yf, g, adw, nwd, yfg);
+          nw0 = FO::add(nwd, adw);
+          dw = dwn;
+        } else {
+          yfg = FO::mul(yf, g);
+        }
+        pt = FO::add(P, FO::add(ci, q));
+        vn = FO::add(vne, yfg);
+        vd = vde;
+        if (i == 0) break;
+      }
+    } else if (!r_root) {
       for (uint32_t i = m - 1; i > calls; --i) {
         T ci, ch;
         coeffs(i, ci, ch);

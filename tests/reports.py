@@ -18,6 +18,10 @@ CONFIGS = {
     "count": dict(kind=0, ctor=lambda: O.Prio3.new_count(), bits=0, length=0, chunk=0),
     "sum8": dict(kind=1, ctor=lambda: O.Prio3.new_sum(8), bits=8, length=0, chunk=0),
     "sum32": dict(kind=1, ctor=lambda: O.Prio3.new_sum(32), bits=32, length=0, chunk=0),
+    # bits not a power of two (calls != m / 2) and the extremes of the Sum query loop
+    "sum5": dict(kind=1, ctor=lambda: O.Prio3.new_sum(5), bits=5, length=0, chunk=0),
+    "sum1": dict(kind=1, ctor=lambda: O.Prio3.new_sum(1), bits=1, length=0, chunk=0),
+    "sum64": dict(kind=1, ctor=lambda: O.Prio3.new_sum(64), bits=64, length=0, chunk=0),
     "sumvec_small": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(2, 10, 3), bits=2, length=10,
                          chunk=3),
     "countvec15": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(1, 15, 3), bits=1, length=15,

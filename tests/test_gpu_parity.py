@@ -12,7 +12,7 @@ from tests.reports import CONFIGS, expected_aggregate, make_batch, plaintext_sum
 
 pytestmark = pytest.mark.gpu
 
-SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
+SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sum5": 24, "sum1": 16, "sum64": 16, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
          "hist256": 24, "sumvec_8_1000": 6, "fp16_3": 12, "fp32_5": 8, "fp64_4": 8, "fp16_300": 6,
          "fp16_5000": 2}
 FPVEC = [k for k in SIZES if k.startswith("fp")]
