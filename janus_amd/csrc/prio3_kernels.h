@@ -1738,6 +1738,74 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_flp_wires for short rows (chunk <= 64, Field128: Histogram, small SumVec/CountVec): a group of
+// G = next_pow2(chunk) lanes per report, lane j = column j, every call k in that lane:
+//   a_j = sum_k MM[k] x_(kc+j),  b_j = sum_k LM[k] x_(kc+j)   (lazy 256-bit MACs, one REDC each)
+// For fixed k the group's x loads are one contiguous 16c-byte run and the weight loads a broadcast;
+// no LDS, no barrier.  Histogram's sum x (for v) is an xor-shuffle reduction inside the group.
+// Same outputs as k_flp_wires, which spends a 64-thread block (4 row groups x 16 columns, LDS
+// partials, three barriers, a one-thread tail) on each Histogram(256) report.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_flp_wires_cols(Cfg cfg, uint32_t n, uint32_t lg, CRows meas,
+                                                        WMat wm, CRows jr, Rows out_prep,
+                                                        uint8_t* status) {
+  using FO = Field128Ops;
+  using T = F128;
+  constexpr size_t ES = 16;
+  const uint32_t G = 1u << lg;
+  const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t r = gt >> lg, j = gt & (G - 1u);
+  const uint32_t rr = r < n ? r : n - 1u;  // dead lanes read a valid row and store nothing
+  const bool live = r < n && status[rr] == ST_OK;
+  const uint32_t C = cfg.calls, c = cfg.chunk;
+  const bool col = live && j < c;
+  const uint8_t* xr = meas.at(rr);
+  Wide wa, wb;
+  wide_zero(wa);
+  wide_zero(wb);
+  T xsum = FO::zero();
+  bool bad = false;
+#pragma unroll 4
+  for (uint32_t k = 0; k < C; ++k) {
+    const uint32_t idx = k * c + j;
+    T x = FO::zero();
+    if (col && idx < cfg.meas_len) {
+      x = FO::load(xr + (size_t)idx * ES);
+      bad |= !FO::is_canonical(x);
+    }
+    const T mm = FO::load(wm.el(rr, k)), lm = FO::load(wm.el(rr, C + k));
+    wide_mac(wa, mm, x);
+    wide_mac(wb, lm, x);
+    if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x);
+  }
+  const T a = wide_reduce(wa), b = wide_reduce(wb);
+  uint8_t* outp = out_prep.at(rr);
+  if (col) {
+    const T rp = FO::load(wm.el(rr, 2 * C + j));  // Montgomery
+    FO::store(outp + (size_t)(1 + 2 * j) * ES,
+              FO::add(FO::load(wm.el(rr, 2 * C + c + j)), FO::mul(rp, a)));
+    FO::store(outp + (size_t)(2 + 2 * j) * ES, FO::add(FO::load(wm.el(rr, 2 * C + 2 * c + j)), b));
+  }
+  if (cfg.kind == KIND_HISTOGRAM) {
+    for (uint32_t sft = G >> 1; sft > 0; sft >>= 1) {
+      xsum = FO::add(xsum, shfl_xor_T<FO>(xsum, (int)sft));
+    }
+  }
+  const uint64_t bm = __ballot(bad);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t gmask = (G >= 64u ? ~0ull : ((1ull << G) - 1ull)) << (lane & ~(G - 1u));
+  if (!live || j != 0u) return;
+  if (cfg.kind == KIND_HISTOGRAM) {
+    // v = jr[1] * range + jr[1]^2 * (sum x - 1/2)
+    const T gsum = FO::load(wm.el(rr, 2 * C + 3 * c));
+    const T r1m = FO::to_mont(FO::load(jr.at(rr) + ES));
+    const T sc = FO::sub(xsum, FO::half());
+    FO::store(outp, FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc)));
+  }
+  if (bm & gmask) status[rr] = ST_INVALID_MESSAGE;
+}
+
+// ------------------------------------------------------------------------------------------------
 // prepare_shares_to_prepare_message (prio): verifier = sum of shares; decide; msg = derive_seed(
 // 0^16, dst6, part_0 || part_1).  decide: v == 0 and G(wires) == p(t),
 //   G = Mul / ParallelSum(Mul): sum_j w_2j w_2j+1 ;  PolyEval(x^2 - x): w^2 - w.
