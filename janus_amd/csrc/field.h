@@ -241,6 +241,25 @@ DEVI F128 inv_mont128(const F128& x) {
 }
 
 // Montgomery-form power x^e (x in Montgomery form, result Montgomery form).
+// x^(p - 2) for Field64 (Montgomery in, Montgomery out): p - 2 = (2^31 - 1) 2^33 + (2^32 - 1),
+// an addition chain of 64 squarings + 9 multiplications (square-and-multiply: 64 + 63).
+DEVI F64 inv_mont64(const F64& x) {
+  using FO = Field64Ops;
+  auto sqn = [](F64 a, int n) {
+    for (int i = 0; i < n; ++i) a = FO::mul(a, a);
+    return a;
+  };
+  const F64 x2 = FO::mul(FO::mul(x, x), x);  // x^(2^2 - 1)
+  const F64 x3 = FO::mul(FO::mul(x2, x2), x);
+  const F64 x6 = FO::mul(sqn(x3, 3), x3);
+  const F64 x12 = FO::mul(sqn(x6, 6), x6);
+  const F64 x24 = FO::mul(sqn(x12, 12), x12);
+  const F64 x30 = FO::mul(sqn(x24, 6), x6);
+  const F64 x31 = FO::mul(FO::mul(x30, x30), x);
+  const F64 x32 = FO::mul(FO::mul(x31, x31), x);
+  return FO::mul(sqn(x31, 33), x32);
+}
+
 template <class FO>
 DEVI typename FO::T mont_pow(typename FO::T x, uint64_t e) {
   typename FO::T r = FO::one_mont();

@@ -959,7 +959,7 @@ DEVI void mul3(const typename FO::T& a0, const typename FO::T& b0, const typenam
 template <class FO>
 DEVI typename FO::T inv_mont(const typename FO::T& x) {
   if constexpr (FO::ES == 16) return inv_mont128(x);
-  else return mont_pow<FO>(x, Field64Ops::P - 2ull);
+  else return inv_mont64(x);
 }
 
 #ifndef FLPQ_WAVES
