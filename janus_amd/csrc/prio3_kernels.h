@@ -2296,7 +2296,8 @@ __global__ void __launch_bounds__(256) k_report_meta_fold(uint32_t nwaves, const
   const uint32_t slot = blockIdx.x;
   uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tmin = ~0ull, tmax = 0ull;
-  for (uint32_t w = threadIdx.x; w < nwaves; w += blockDim.x) {
+  for (uint32_t w = blockIdx.y * blockDim.x + threadIdx.x; w < nwaves;
+       w += blockDim.x * gridDim.y) {
     const WaveMeta& p = partial[w];
     if (p.slot != slot) continue;
 #pragma unroll
