@@ -1074,23 +1074,24 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
           mul3<FO>(tmm, ch, rm, twi, rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)i * calls) % m)), q,
                    y, u);
         }
-        // triple 2: P = t pt, and for wire iterations a = alpha^i x, dw d
-        if (wire) {
-          mul3<FO>(tm, pt, twi, x, dw, d, P, a, dwn);
-        } else {
-          P = FO::mul(tm, pt);
-        }
-        if (!half) g = FO::mul(FO::sub(u, one), vd);
         const T e = FO::sub(y, one);
-        // triple 3: y f, vd e, vn e
-        mul3<FO>(y, f, vd, e, vn, e, yf, vde, vne);
         if (wire) {
-          // triple 4: a dw, nw0 d, (y f) g
+          // P = t pt, a = alpha^i x, dw d;  y f, vd e, vn e;  a dw, nw0 d, (y f) g
+          mul3<FO>(tm, pt, twi, x, dw, d, P, a, dwn);
+          if (!half) g = FO::mul(FO::sub(u, one), vd);
+          mul3<FO>(y, f, vd, e, vn, e, yf, vde, vne);
           mul3<FO>(a, dw, nw0, d, yf, g, adw, nwd, yfg);
           nw0 = FO::add(nwd, adw);
           dw = dwn;
+        } else if (half) {
+          // y f, vd e, vn e;  P = t pt, (y f) g (+ an idle slot: still cheaper than two singles)
+          mul3<FO>(y, f, vd, e, vn, e, yf, vde, vne);
+          T idle;
+          mul3<FO>(tm, pt, yf, g, one, one, P, yfg, idle);
         } else {
-          yfg = FO::mul(yf, g);
+          // g = (yc - 1) vd, P = t pt, y f;  vd e, vn e, (y f) g
+          mul3<FO>(FO::sub(u, one), vd, tm, pt, y, f, g, P, yf);
+          mul3<FO>(vd, e, vn, e, yf, g, vde, vne, yfg);
         }
         pt = FO::add(P, FO::add(ci, q));
         vn = FO::add(vne, yfg);
@@ -1765,7 +1766,6 @@ __global__ void __launch_bounds__(256) k_flp_wires_cols(Cfg cfg, uint32_t n, uin
   wide_zero(wb);
   T xsum = FO::zero();
   bool bad = false;
-#pragma unroll 4
   for (uint32_t k = 0; k < C; ++k) {
     const uint32_t idx = k * c + j;
     T x = FO::zero();
