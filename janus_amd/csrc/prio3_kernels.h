@@ -983,7 +983,20 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
   const T one = FO::one_mont();
   const T tm = FO::to_mont(FO::load(tq.at(r)));
   T tmm = tm;
-  for (uint32_t i = 0; i < cfg.logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
+  // Sum: t^m, r^m and r^calls (calls < m, right-to-left square-and-multiply) advance together,
+  // one triple of squarings per bit
+  T rm = FO::zero(), rmm = FO::zero(), rc = one;
+  if (cfg.kind == KIND_SUM) {
+    rm = FO::to_mont(FO::load(jr.at(r)));
+    rmm = rm;
+    T b = rm;
+    for (uint32_t q = 0; q < cfg.logm; ++q) {
+      if ((calls >> q) & 1u) rc = FO::mul(rc, b);
+      mul3<FO>(tmm, tmm, rmm, rmm, b, b, tmm, rmm, b);
+    }
+  } else {
+    for (uint32_t i = 0; i < cfg.logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
+  }
   const bool root = FO::eq(tmm, one);
   const T cm = FO::mul(FO::sub(tmm, one), ld_tw<FO>(cfg, m));  // (t^m - 1)/m, Montgomery
 
@@ -1028,10 +1041,6 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
     // (Horner on p(t) = sum_i (c_i + c_(i+m) t^m) t^i, the v fraction over G(r alpha^i), and for
     // i <= calls the wire fraction), so the Montgomery carry chains of one fill the other's
     // hazard slots; y_i = r alpha^i == 1 needs r^m == 1, handled outside the loop.
-    const T rm = FO::to_mont(FO::load(jr.at(r)));
-    const T rc = mont_pow<FO>(rm, calls);  // r^calls
-    T rmm = rm;
-    for (uint32_t q = 0; q < cfg.logm; ++q) rmm = FO::mul(rmm, rmm);
     const bool r_root = FO::eq(rmm, one);
     auto coeffs = [&](uint32_t i, T& ci, T& ch) {
       ci = FO::load(gp + (size_t)i * ES);
