@@ -9,8 +9,9 @@ RCCL all-gather + mod-p merge of both aggregators' per-GPU partial aggregate sha
 (decrypted shares, SURVEY.md §8(d) recipe) are resident in HBM before timing starts; HPKE is out of
 scope.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]  (N > 1 via torch.distributed.run).
-Prints one JSON line on rank 0.
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1: bench.py starts the N ranks itself
+(a child `torch.distributed.run`, one process per GPU), or runs as one rank of an outside launcher
+whose WORLD_SIZE must equal N (a mismatch is an error).  Prints one JSON line on rank 0.
 """
 import argparse
 import ctypes
@@ -194,6 +195,31 @@ def oracle_transcript_gate(vdaf, kind, bits, length, chunk, vk, syn, d_pub, d_li
             f"== Python oracle run_vdaf (XofTurboShake128)")
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_argv(n: int, argv, port: int):
+    """The child command that runs this bench as n ranks on one node (Janus scales the same
+    path by running aggregation jobs concurrently, aggregator/src/binary_utils/job_driver.rs:
+    119-216; here each rank owns one GPU and a contiguous report range)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Run the n-rank bench as a child process (rank 0's JSON line goes straight to our stdout)
+    and return its exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this host driver
+    return subprocess.run(launcher_argv(n, argv, free_port()), env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,13 +253,22 @@ def main():
                          "max_concurrent_job_workers)")
     args = ap.parse_args()
 
+    # One process per GPU.  `--gpus N` without a launcher: start the N ranks ourselves, as a
+    # child torch.distributed.run (never exec: nothing here has touched the GPU yet, and the
+    # parent only relays).  Under a launcher, WORLD_SIZE must be N.
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU "
+              f"(or drop --gpus and let bench.py start them)", file=sys.stderr)
+        sys.exit(2)
+
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     # the device of this rank (gloo rehearsal: ranks may share GPUs)
     gpu = local_rank % max(1, torch.cuda.device_count()) if args.merge == "gloo" else local_rank
     torch.cuda.set_device(gpu)
@@ -812,6 +847,8 @@ def main():
         "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
         "parity": parity,
         "gen_seconds": round(gen_s, 1),
+        # the engine build that ran: SHA-256 of its sources + flags (janus_amd/_lib.py)
+        "build_hash": L.prio3gpu_build_hash().decode(),
     }
     if cpu:
         out["speedup_vs_cpu"] = round(value / cpu["value"], 1)

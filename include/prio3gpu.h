@@ -136,7 +136,10 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
 /* Work queued on `ctx` from now on starts only after all work queued on `other` so far. */
 int prio3gpu_ctx_wait(prio3gpu_ctx* ctx, prio3gpu_ctx* other);
 /* The same in two steps: mark what is queued on `ctx` now; later make another context wait for
- * that mark.  Marks live in a ring of 16 per context: wait on a mark before 16 newer ones. */
+ * that mark.  Marks live in a ring of 16 per context, each carrying a generation: waiting on a mark
+ * after 16 newer ones were taken fails with PRIO3GPU_E_ARG ("stale mark") instead of waiting on
+ * newer work.  prio3gpu_ctx_wait uses a private event and takes no mark.  Marking and waiting are
+ * thread-safe per context. */
 int prio3gpu_ctx_mark(prio3gpu_ctx* ctx, int* out_mark);
 int prio3gpu_ctx_wait_mark(prio3gpu_ctx* ctx, prio3gpu_ctx* other, int mark);
 /* The context's HIP stream (hipStream_t), for callers that interoperate (e.g. bench timing). */
@@ -443,6 +446,10 @@ int prio3gpu_hpke_open_report_shares(const uint8_t* task_id, const prio3gpu_hpke
 
 /* Last error message for this thread (static storage). */
 const char* prio3gpu_last_error(void);
+/* Build identity: the SHA-256 (hex) of the sources, headers and compiler flags the library was
+ * built from ("unhashed" for a build outside janus_amd/_lib.py).  A caller (the Rust build.rs,
+ * janus_amd/_lib.py) rejects a library whose hash is not that of the sources it ships with. */
+const char* prio3gpu_build_hash(void);
 
 #ifdef __cplusplus
 }

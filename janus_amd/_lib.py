@@ -37,19 +37,53 @@ class EmptyAggregation(Prio3GpuError):
 
 E_INVALID_MESSAGE = -7
 
+SOURCES = ("engine.hip", "codec.cpp", "hpke.cpp")
+FLAGS = ("--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared")
+LIBS = ("-lrccl", "-lcrypto")
+HASH_MARKER = b"PRIO3GPU_BUILD_HASH="
+
+
+def source_hash(csrc: Path = CSRC, include: Path = INCLUDE, flags=FLAGS) -> str:
+    """SHA-256 (hex) over the engine's sources, its headers and the compiler flags: the build key
+    (file mtimes are not: a tree copied to another machine keeps its library only if the
+    contents it was built from are unchanged)."""
+    import hashlib
+    h = hashlib.sha256()
+    files = [csrc / s for s in SOURCES] + sorted(csrc.glob("*.h")) + [include / "prio3gpu.h"]
+    for p in files:
+        h.update(p.name.encode() + b"\0" + p.read_bytes() + b"\0")
+    h.update(" ".join(flags + LIBS).encode())
+    return h.hexdigest()
+
+
+def embedded_hash(path: Path = LIB_PATH):
+    """The build hash a library carries (its `prio3gpu_build_id` marker), read from the file
+    without loading it; None if the file is missing or carries no marker (a foreign library)."""
+    try:
+        data = Path(path).read_bytes()
+    except OSError:
+        return None
+    i = data.find(HASH_MARKER)
+    if i < 0:
+        return None
+    j = data.find(b"\0", i)
+    return data[i + len(HASH_MARKER):j].decode(errors="replace")
+
+
+def needs_rebuild(path: Path = LIB_PATH, want=None) -> bool:
+    return embedded_hash(path) != (want or source_hash())
+
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile the HIP engine for gfx950 into janus_amd/lib/libprio3gpu.so."""
-    srcs = [CSRC / "engine.hip", CSRC / "codec.cpp", CSRC / "hpke.cpp"]
-    deps = srcs + list(CSRC.glob("*.h")) + [INCLUDE / "prio3gpu.h"]
-    if LIB_PATH.exists() and not force:
-        newest = max(p.stat().st_mtime for p in deps)
-        if LIB_PATH.stat().st_mtime >= newest:
-            return LIB_PATH
+    """Compile the HIP engine for gfx950 into janus_amd/lib/libprio3gpu.so, unless the library
+    there was built from exactly these sources and flags (its embedded build hash)."""
+    want = source_hash()
+    if not force and not needs_rebuild(LIB_PATH, want):
+        return LIB_PATH
     LIB_DIR.mkdir(exist_ok=True)
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", str(tmp)] + [str(x) for x in srcs] + ["-lrccl", "-lcrypto"]
+    cmd = (["hipcc"] + list(FLAGS) + [f'-DPRIO3GPU_BUILD_HASH="{want}"', "-o", str(tmp)]
+           + [str(CSRC / s) for s in SOURCES] + list(LIBS))
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -104,6 +138,7 @@ def _declare(lib):
         "prio3gpu_dev_free": (c.c_int, [P, P]),
         "prio3gpu_memcpy": (c.c_int, [P, P, P, c.c_size_t]),
         "prio3gpu_last_error": (c.c_char_p, []),
+        "prio3gpu_build_hash": (c.c_char_p, []),
         "prio3gpu_unshard": (c.c_int, [P, u8p, c.c_size_t, c.c_uint64, u8p, P]),
         # DAP codec edge (host-only, codec.cpp)
         "prio3gpu_decode_agg_init_req": (c.c_int, [u8p, c.c_size_t, c.c_int, u8p, P, P, c.c_size_t,
@@ -161,7 +196,7 @@ EXPORTED = [
     "prio3gpu_random_size", "prio3gpu_shard", "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
     "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
     "prio3gpu_prof_kernel_name", "prio3gpu_test_squeeze", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
-    "prio3gpu_last_error", "prio3gpu_unshard", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
+    "prio3gpu_last_error", "prio3gpu_build_hash", "prio3gpu_unshard", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
     "prio3gpu_apply_faults", "prio3gpu_check_agg_init_req", "prio3gpu_batch_aggregation_merge",
     "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",
     "prio3gpu_encode_agg_init_req", "prio3gpu_decode_agg_job_resp", "prio3gpu_gather_helper_resps",
@@ -176,6 +211,11 @@ def lib():
     if _lib is None:
         if not LIB_PATH.exists():
             raise Prio3GpuError(f"HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+        if not os.environ.get("PRIO3GPU_LIB"):  # A/B variants name their own build
+            got, want = embedded_hash(LIB_PATH), source_hash()
+            if got != want:
+                raise Prio3GpuError(f"stale or foreign library {LIB_PATH}: build hash {got} is "
+                                    f"not the sources' {want} (run __graft_entry__.build())")
         try:
             l = ctypes.CDLL(str(LIB_PATH))
         except OSError as e:

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <string>
 #include <initializer_list>
+#include <mutex>
 #include <vector>
 
 #include "../../include/prio3gpu.h"
@@ -209,7 +210,11 @@ struct prio3gpu_ctx {
   bool async_mode = false;
   static constexpr int kMarks = 16;
   hipEvent_t ev[kMarks] = {};  // ring of marks (prio3gpu_ctx_mark)
+  uint32_t ev_gen[kMarks] = {};  // generation of each ring slot: a mark = gen * kMarks + slot
   int ev_next = 0;
+  uint32_t gen_next = 1;
+  hipEvent_t wait_ev = nullptr;  // prio3gpu_ctx_wait: recorded on the other context, not a mark
+  std::mutex mark_mu;            // ev_next / ev_gen / wait_ev
   // the device-side accumulation plan of the last call (single slot, no per-report slots):
   // reused while (n, speculative layout, slot count) are unchanged -- no host planning, no upload
   bool plan_valid = false;
@@ -1017,26 +1022,6 @@ int launch_out_shares(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8
 
 bool is_f64(const prio3gpu_ctx* c) { return c->cfg.es == 8; }
 
-// Device slot meta (SHA-256 state words, [tmin, tmax]) <-> host BatchAggregation fields.
-prio3gpu_batch_aggregation slot_meta_to_ba(const SlotMeta& m) {
-  prio3gpu_batch_aggregation b{};
-  for (int i = 0; i < 8; ++i)
-    for (int k = 0; k < 4; ++k) b.checksum[4 * i + k] = (uint8_t)(m.ck[i] >> (24 - 8 * k));
-  if (m.tmin <= m.tmax) {
-    b.interval_start = m.tmin;
-    b.interval_duration = m.tmax - m.tmin + 1;
-  }
-  return b;
-}
-SlotMeta ba_to_slot_meta(const prio3gpu_batch_aggregation& b) {
-  SlotMeta m{};
-  for (int i = 0; i < 8; ++i)
-    m.ck[i] = ((uint32_t)b.checksum[4 * i] << 24) | ((uint32_t)b.checksum[4 * i + 1] << 16) |
-              ((uint32_t)b.checksum[4 * i + 2] << 8) | b.checksum[4 * i + 3];
-  m.tmin = b.interval_duration ? b.interval_start : ~0ull;
-  m.tmax = b.interval_duration ? b.interval_start + b.interval_duration - 1 : 0ull;
-  return m;
-}
 
 int check_state(prio3gpu_ctx* c, prio3gpu_state* st, size_t n) {
   if (!c || !st || st->ctx != c) {
@@ -1082,9 +1067,20 @@ int finish_call(prio3gpu_ctx* c, std::initializer_list<const void*> bufs) {
 // =================================================================================================
 // C ABI
 // =================================================================================================
+// Build identity: janus_amd/_lib.py passes the SHA-256 of the sources, headers and flags it
+// compiled; it is kept as a searchable marker so a stale or foreign library is detected without
+// loading it.
+#ifndef PRIO3GPU_BUILD_HASH
+#define PRIO3GPU_BUILD_HASH "unhashed"
+#endif
+extern "C" __attribute__((used)) const char prio3gpu_build_id[] =
+    "PRIO3GPU_BUILD_HASH=" PRIO3GPU_BUILD_HASH;
+
 extern "C" {
 
 const char* prio3gpu_last_error(void) { return g_err.c_str(); }
+
+const char* prio3gpu_build_hash(void) { return prio3gpu_build_id + 20; }
 
 int prio3gpu_ctx_create(int kind, uint32_t bits, uint32_t length, uint32_t chunk_length,
                         const uint8_t verify_key[16], int device, prio3gpu_ctx** out) {
@@ -1172,6 +1168,7 @@ int prio3gpu_ctx_destroy(prio3gpu_ctx* c) {
   for (auto ev : c->prof.pool) (void)hipEventDestroy(ev);
   for (auto ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -1382,8 +1379,8 @@ int prio3gpu_agg_update_reports(prio3gpu_agg* a, size_t n, const uint8_t* report
                        reinterpret_cast<SlotMeta*>(a->meta.p));
   }
   HIPCHK(hipGetLastError());
-  if (!is_device_ptr(report_ids) || !is_device_ptr(times)) HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  // every staged host buffer (ids, times, status, slots) must outlive its copy: the async rule
+  return finish_call(c, {report_ids, times, status, batch_slots});
 }
 
 int prio3gpu_agg_read_reports(prio3gpu_agg* a, uint32_t slot, uint8_t* out_checksum,
@@ -1520,21 +1517,34 @@ int prio3gpu_ctx_mark(prio3gpu_ctx* c, int* out_mark) {
     return PRIO3GPU_E_ARG;
   }
   HIPCHK(hipSetDevice(c->device));
+  constexpr int K = prio3gpu_ctx::kMarks;
+  std::lock_guard<std::mutex> lk(c->mark_mu);
   const int k = c->ev_next;
-  c->ev_next = (c->ev_next + 1) % prio3gpu_ctx::kMarks;
   if (!c->ev[k]) HIPCHK(hipEventCreateWithFlags(&c->ev[k], hipEventDisableTiming));
   HIPCHK(hipEventRecord(c->ev[k], c->stream));
-  *out_mark = k;
+  c->ev_next = (k + 1) % K;
+  const uint32_t gen = c->gen_next;
+  c->gen_next = (gen + 1) & 0x07FFFFFFu ? (gen + 1) & 0x07FFFFFFu : 1u;  // mark stays a positive int
+  c->ev_gen[k] = gen;
+  *out_mark = (int)(gen * (uint32_t)K + (uint32_t)k);
   return 0;
 }
 
 int prio3gpu_ctx_wait_mark(prio3gpu_ctx* c, prio3gpu_ctx* other, int mark) {
-  if (!c || !other || mark < 0 || mark >= prio3gpu_ctx::kMarks || !other->ev[mark]) {
+  constexpr int K = prio3gpu_ctx::kMarks;
+  if (!c || !other || mark < K) {
     set_err("bad mark");
     return PRIO3GPU_E_ARG;
   }
+  const int k = mark % K;
+  const uint32_t gen = (uint32_t)(mark / K);
+  std::lock_guard<std::mutex> lk(other->mark_mu);
+  if (!other->ev[k] || other->ev_gen[k] != gen) {
+    set_err("stale mark %d: its ring slot was re-marked (more than %d newer marks)", mark, K);
+    return PRIO3GPU_E_ARG;
+  }
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamWaitEvent(c->stream, other->ev[mark], 0));
+  HIPCHK(hipStreamWaitEvent(c->stream, other->ev[k], 0));
   return 0;
 }
 
@@ -1544,9 +1554,14 @@ int prio3gpu_ctx_wait(prio3gpu_ctx* c, prio3gpu_ctx* other) {
     return PRIO3GPU_E_ARG;
   }
   if (c == other) return 0;
-  int m = 0;
-  CHK(prio3gpu_ctx_mark(other, &m));
-  return prio3gpu_ctx_wait_mark(c, other, m);
+  HIPCHK(hipSetDevice(c->device));
+  // a private event of the waiting context, recorded on the other stream: the other context's
+  // mark ring (marks its caller may still hold) is not touched
+  std::lock_guard<std::mutex> lk(c->mark_mu);
+  if (!c->wait_ev) HIPCHK(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(c->wait_ev, other->stream));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->wait_ev, 0));
+  return 0;
 }
 
 int prio3gpu_prepare_shares_to_prepare_message(prio3gpu_ctx* c, size_t n,
@@ -1881,60 +1896,38 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
   CHK(cm->mgather.ensure(mbytes * cm->nranks));
   RCCLCHK(ncclAllGather(local->meta.p, cm->mgather.p, mbytes, ncclUint8, cm->comm, c->stream));
   prio3gpu_agg* dst = total ? total : local;
-  if (!total) HIPCHK(hipMemsetAsync(local->share.p, 0, bytes, c->stream));
-  // dst += sum over ranks, in rank order (identical on every rank; mod-p addition is exact)
-  for (int r = 0; r < cm->nranks; ++r) {
-    const uint8_t* src = cm->gather.u8() + (size_t)r * bytes;
-    {
-      PROF(KID_MERGE);
-      if (is_f64(c))
-        hipLaunchKernelGGL(k_merge<Field64Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
-                           dst->share.u8(), src, nel);
-      else
-        hipLaunchKernelGGL(k_merge<Field128Ops>, grid1(nel, 256), dim3(256), 0, c->stream,
-                           dst->share.u8(), src, nel);
-    }
+  // ONE stream-ordered launch folds every rank, in rank order (identical on every rank; mod-p
+  // addition is exact): dst = (total ? dst : 0) + sum_r share_r, counts likewise, and the slot
+  // meta = BatchAggregation::merged_with's checksum XOR + interval union
+  // (models.rs:962-991; core/src/time.rs:289-302).  No host round trip: in async mode the call
+  // returns once queued, like every other all-device call.
+  {
+    PROF(KID_MERGE);
+    const uint32_t nb = (uint32_t)std::min<size_t>((nel + 255) / 256, 4096);
+    if (is_f64(c))
+      hipLaunchKernelGGL(k_merge_ranks<Field64Ops>, dim3(nb + 1), dim3(256), 0, c->stream,
+                         dst->share.u8(), cm->gather.u8(), nel, (uint32_t)cm->nranks,
+                         total ? 1u : 0u, reinterpret_cast<unsigned long long*>(dst->counts.p),
+                         reinterpret_cast<const unsigned long long*>(cm->cgather.p),
+                         reinterpret_cast<SlotMeta*>(dst->meta.p),
+                         reinterpret_cast<const SlotMeta*>(cm->mgather.p), local->slots, nb);
+    else
+      hipLaunchKernelGGL(k_merge_ranks<Field128Ops>, dim3(nb + 1), dim3(256), 0, c->stream,
+                         dst->share.u8(), cm->gather.u8(), nel, (uint32_t)cm->nranks,
+                         total ? 1u : 0u, reinterpret_cast<unsigned long long*>(dst->counts.p),
+                         reinterpret_cast<const unsigned long long*>(cm->cgather.p),
+                         reinterpret_cast<SlotMeta*>(dst->meta.p),
+                         reinterpret_cast<const SlotMeta*>(cm->mgather.p), local->slots, nb);
   }
   HIPCHK(hipGetLastError());
-  // counts
-  std::vector<unsigned long long> sum(local->slots), cur(local->slots);
-  HIPCHK(hipMemcpyAsync(sum.data(), cm->cgather.p, local->slots * 8, hipMemcpyDeviceToHost,
-                        c->stream));
-  HIPCHK(hipMemcpyAsync(cur.data(), dst->counts.p, local->slots * 8, hipMemcpyDeviceToHost,
-                        c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  for (uint32_t s = 0; s < local->slots; ++s) cur[s] = (total ? cur[s] : 0ull) + sum[s];
-  std::vector<SlotMeta> mg((size_t)local->slots * cm->nranks), md(local->slots);
-  HIPCHK(hipMemcpy(mg.data(), cm->mgather.p, mbytes * cm->nranks, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(md.data(), dst->meta.p, mbytes, hipMemcpyDeviceToHost));
-  // checksum XOR + interval union in rank order: BatchAggregation::merged_with's host half
-  // (prio3gpu_batch_aggregation_merge; the shares were merged on the GPU above, counts by RCCL)
-  for (uint32_t s = 0; s < local->slots; ++s) {
-    prio3gpu_batch_aggregation acc = total ? slot_meta_to_ba(md[s]) : slot_meta_to_ba(SlotMeta{
-                                                                          {0}, ~0ull, 0ull});
-    for (int r = 0; r < cm->nranks; ++r) {
-      const prio3gpu_batch_aggregation x = slot_meta_to_ba(mg[(size_t)r * local->slots + s]);
-      CHK(prio3gpu_batch_aggregation_merge(c->cfg.es, 0, &acc, &x));
-    }
-    md[s] = ba_to_slot_meta(acc);
-  }
-  HIPCHK(hipMemcpyAsync(dst->meta.p, md.data(), mbytes, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(dst->counts.p, cur.data(), local->slots * 8, hipMemcpyHostToDevice,
-                        c->stream));
-  if (total) {  // the local partial has been merged: reset it for the next job
+  if (total) {  // the local partial has been merged: reset it for the next job (flush semantics)
     HIPCHK(hipMemsetAsync(local->share.p, 0, bytes, c->stream));
     HIPCHK(hipMemsetAsync(local->counts.p, 0, (size_t)local->slots * 8, c->stream));
-    std::vector<SlotMeta> z(local->slots);
-    for (auto& x : z) {
-      memset(x.ck, 0, sizeof x.ck);
-      x.tmin = ~0ull;
-      x.tmax = 0ull;
-    }
-    HIPCHK(hipMemcpyAsync(local->meta.p, z.data(), mbytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));  // z lives on this stack frame
+    hipLaunchKernelGGL(k_meta_reset, dim3((local->slots + 255) / 256), dim3(256), 0, c->stream,
+                       reinterpret_cast<SlotMeta*>(local->meta.p), local->slots);
+    HIPCHK(hipGetLastError());
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  return finish_call(c, {});
 }
 
 }  // extern "C"

@@ -102,6 +102,30 @@ struct SqueezeVec;
 // exact per-element path (prio's rejection sampling), so the output is the same either way.
 DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 
+// A fast block's element stores, deferred into the next permutation: the Keccak hook issues store
+// k after round 12 + k, so the block's 10-11 per-lane-row stores (64 rows per wave-instruction)
+// reach the memory pipeline spread over the permutation rather than as one burst the wave waits
+// behind (k_expand, PRIO3GPU build flag P3G_EXPAND_DEFER).
+struct PendingStores {
+  ulonglong2 v[11];
+  ulonglong2* base = nullptr;
+  uint32_t cnt = 0;  // 0, 10 or 11 pending elements
+  template <int R>
+  static constexpr bool active() { return R >= 12 && R < 23; }
+  template <int R>
+  DEVI void after() {  // store k = R - 12, between the rounds (keccak_fence on both sides)
+    constexpr int k = R - 12;
+    if ((uint32_t)k < cnt) base[k] = v[k];
+    if constexpr (k == 10) cnt = 0;
+  }
+  DEVI void flush() {
+#pragma unroll
+    for (int k = 0; k < 11; ++k)
+      if ((uint32_t)k < cnt) base[k] = v[k];
+    cnt = 0;
+  }
+};
+
 template <>
 struct SqueezeVec<Field128Ops> {
   template <class Next>
@@ -200,6 +224,77 @@ DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out, const Xof& x, bo
   SqueezeVec<FO>::run(s, n, out, exact, KeccakNext{x});
 }
 
+// SqueezeVec<Field128Ops>'s loop with the fast path's stores deferred into the next permutation
+// (PendingStores).  Same output as squeeze_vec: a block whose elements are not all provably
+// canonical takes the exact per-element path, stored at once.
+DEVI void squeeze_vec_f128_deferred(uint64_t s[25], uint32_t n, uint8_t* out, const Xof& x) {
+  using FO = Field128Ops;
+  PendingStores pend;
+  uint32_t cnt = 0, parity = 0;
+  uint64_t carry = 0;
+  while (true) {
+    bool fast = cnt + 11u <= n;
+    if (parity == 0) {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 1]);
+    } else {
+      fast &= hi_ok(s[0]);
+#pragma unroll
+      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
+    }
+    if (fast) {
+      pend.base = reinterpret_cast<ulonglong2*>(out + (size_t)cnt * 16);
+      if (parity == 0) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) pend.v[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
+        carry = s[20];
+        pend.cnt = 10u;
+        cnt += 10u;
+      } else {
+        pend.v[0] = make_ulonglong2(carry, s[0]);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) pend.v[k + 1] = make_ulonglong2(s[2 * k + 1], s[2 * k + 2]);
+        pend.cnt = 11u;
+        cnt += 11u;
+      }
+    } else if (parity == 0) {
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
+        if (cnt < n && FO::is_canonical(e)) {
+          FO::store(out + (size_t)cnt * 16, e);
+          ++cnt;
+        }
+      }
+      carry = s[20];
+    } else {
+      {
+        F128 e = FO::from_u64x2(carry, s[0]);
+        if (cnt < n && FO::is_canonical(e)) {
+          FO::store(out + (size_t)cnt * 16, e);
+          ++cnt;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
+        if (cnt < n && FO::is_canonical(e)) {
+          FO::store(out + (size_t)cnt * 16, e);
+          ++cnt;
+        }
+      }
+    }
+    if (cnt >= n) break;
+    parity ^= 1u;
+    keccak_x_h(s, x, pend);
+  }
+  pend.flush();
+}
+
+#ifndef P3G_EXPAND_DEFER
+#define P3G_EXPAND_DEFER 0
+#endif
+
 // XOF(seed, dst(usage), binder=[byte]) expanded into n elements (helper share expansion).
 template <class FO>
 DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed_lo,
@@ -212,7 +307,12 @@ DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed
   m.pad(26, x);
   uint64_t s[25];
   sponge_one_block(s, m, x);
-  squeeze_vec<FO>(s, n, out, x, exact);
+  if constexpr (P3G_EXPAND_DEFER != 0 && FO::ES == 16) {
+    if (!exact) squeeze_vec_f128_deferred(s, n, out, x);
+    else squeeze_vec<FO>(s, n, out, x, exact);
+  } else {
+    squeeze_vec<FO>(s, n, out, x, exact);
+  }
 }
 
 // derive_seed(0^16, dst6, part0 || part1)   (prio Prio3::derive_joint_rand_seed)
@@ -359,6 +459,24 @@ DEVI void acc_u64(uint32_t& lo, uint32_t& hi, uint32_t& cy, uint64_t x) {
       : "vcc");
 }
 
+#ifndef P3G_JR_SPREAD
+#define P3G_JR_SPREAD 0
+#endif
+// P3G_JR_SPREAD: k_jr issues the 11 LDS-DMA pieces of the next window one per round (rounds
+// 12..22) inside the permutation instead of as one burst before it.
+template <class SP>
+struct SpreadHook {
+  SP* sp;
+  int64_t b;
+  bool on;
+  template <int R>
+  static constexpr bool active() { return R >= 12 && R < 23; }
+  template <int R>
+  DEVI void after() {
+    if (on) (*sp)(b, R - 12);
+  }
+};
+
 constexpr uint32_t kJrWin = 176;  // bytes per report in the LDS window (22 words)
 constexpr uint32_t kJrWaveLds = 64 * kJrWin;
 
@@ -393,24 +511,27 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
   const uint32_t mstride = (uint32_t)meas.stride;
   const uint8_t* wbase = meas.base + (size_t)r0w * meas.stride;
   auto is_fast = [&](int64_t b) { return (b >= 1) && (21 * b + 15 < nd) && (21 * b + 20 < padw); };
-  auto stage = [&](int64_t b) {  // window <- words [21b-6, 21b+16) of every row of the wave
+  // one LDS-DMA piece q (1 KB: 64 lanes x 16 B) of the window of block b
+  auto stage_piece = [&](int64_t b, int q) {
     const uint8_t* src = wbase + 8 * (21 * b - 6);
     // opaque copies: keep LICM from hoisting the 11 per-lane offsets out of the loop
     uint32_t la, lb;
     asm volatile("v_mov_b32 %0, %1" : "=v"(la) : "v"(la0));
     asm volatile("v_mov_b32 %0, %1" : "=v"(lb) : "v"(lb0));
-#pragma unroll
-    for (int q = 0; q < 11; ++q) {
-      const uint32_t cq = (64u * q) / 11u, dq = (64u * q) % 11u;  // 64q = 11 cq + dq
-      const uint32_t t = lb + dq;
-      const uint32_t wrap = t >= 11u ? 1u : 0u;
-      const uint32_t row = min(la + cq + wrap, rlim);
-      const uint32_t k = t - 11u * wrap;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(src + (row * mstride + 16u * k)),
-          (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, 0, 0);
-    }
+    const uint32_t cq = (64u * q) / 11u, dq = (64u * q) % 11u;  // 64q = 11 cq + dq
+    const uint32_t t = lb + dq;
+    const uint32_t wrap = t >= 11u ? 1u : 0u;
+    const uint32_t row = min(la + cq + wrap, rlim);
+    const uint32_t k = t - 11u * wrap;
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(src + (row * mstride + 16u * k)),
+        (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, 0, 0);
   };
+  auto stage = [&](int64_t b) {  // window <- words [21b-6, 21b+16) of every row of the wave
+#pragma unroll
+    for (int q = 0; q < 11; ++q) stage_piece(b, q);
+  };
+
 
   uint64_t s[25];
 #pragma unroll
@@ -491,11 +612,18 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
         s[w] ^= v;
       }
     }
-    if (is_fast(b + 1)) {  // refill the window (its reads above have completed) under the permutation
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      stage(b + 1);
+    if constexpr (P3G_JR_SPREAD != 0) {
+      const bool refill = is_fast(b + 1);  // wave-uniform
+      if (refill) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      SpreadHook<decltype(stage_piece)> hook{&stage_piece, b + 1, refill};
+      keccak_x_h(s, cfg.xof, hook);
+    } else {
+      if (is_fast(b + 1)) {  // refill the window (its reads above have completed) under the permutation
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stage(b + 1);
+      }
+      keccak_x(s, cfg.xof);
     }
-    keccak_x(s, cfg.xof);
   }
   if (!live) return;
   const uint64_t plo = s[0], phi = s[1];
@@ -2335,6 +2463,60 @@ __global__ void __launch_bounds__(256) k_merge(uint8_t* dst, const uint8_t* src,
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nelems) return;
   FO::store(dst + i * FO::ES, FO::add(FO::load(dst + i * FO::ES), FO::load(src + i * FO::ES)));
+}
+
+// The RCCL flush in one launch (prio3gpu_agg_allreduce): blocks [0, nb) grid-stride over the
+// nelems aggregate elements, dst[i] = (accumulate ? dst[i] : 0) + sum over ranks r of
+// gathered[r * nelems + i] in rank order; block nb folds the slots: counts (already summed by
+// RCCL) and the all-gathered slot meta, checksum XOR + interval union per slot
+// (BatchAggregation::merged_with, aggregator_core/src/datastore/models.rs:962-991).
+template <class FO>
+__global__ void __launch_bounds__(256) k_merge_ranks(uint8_t* dst, const uint8_t* gathered,
+                                                     size_t nelems, uint32_t nranks,
+                                                     uint32_t accumulate,
+                                                     unsigned long long* counts,
+                                                     const unsigned long long* count_sums,
+                                                     SlotMeta* meta, const SlotMeta* gmeta,
+                                                     uint32_t nslots, uint32_t nb) {
+  if (blockIdx.x < nb) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nelems;
+         i += (size_t)nb * blockDim.x) {
+      typename FO::T acc = accumulate ? FO::load(dst + i * FO::ES) : FO::zero();
+      for (uint32_t r = 0; r < nranks; ++r)
+        acc = FO::add(acc, FO::load(gathered + ((size_t)r * nelems + i) * FO::ES));
+      FO::store(dst + i * FO::ES, acc);
+    }
+    return;
+  }
+  for (uint32_t s = threadIdx.x; s < nslots; s += blockDim.x) {
+    counts[s] = (accumulate ? counts[s] : 0ull) + count_sums[s];
+    SlotMeta m;
+    if (accumulate) {
+      m = meta[s];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m.ck[i] = 0u;
+      m.tmin = ~0ull;
+      m.tmax = 0ull;
+    }
+    for (uint32_t r = 0; r < nranks; ++r) {
+      const SlotMeta& x = gmeta[(size_t)r * nslots + s];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m.ck[i] ^= x.ck[i];
+      m.tmin = x.tmin < m.tmin ? x.tmin : m.tmin;  // an empty interval is tmin > tmax
+      m.tmax = x.tmax > m.tmax ? x.tmax : m.tmax;
+    }
+    meta[s] = m;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_meta_reset(SlotMeta* meta, uint32_t nslots) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) meta[s].ck[i] = 0u;
+  meta[s].tmin = ~0ull;
+  meta[s].tmax = 0ull;
 }
 
 }  // namespace p3g

@@ -34,7 +34,7 @@ import numpy as np
 
 from . import codec as C
 from . import hpke
-from ._lib import EmptyAggregation
+from ._lib import EmptyAggregation, Prio3GpuError
 from .prio3 import AggregateShares, Prio3Gpu
 
 
@@ -155,18 +155,40 @@ class HelperAggregateInit:
     def handle(self, req_bytes: bytes, agg: AggregateShares) -> bytes:
         return self.prepare(self.open(req_bytes), agg)
 
-    def handle_jobs(self, reqs: Sequence[bytes], agg: AggregateShares) -> List[bytes]:
-        """Pipelined: host decode + HPKE of job k + 1 overlaps the GPU preparation of job k."""
-        out: List[bytes] = []
+    def handle_jobs(self, reqs: Sequence[bytes], agg: AggregateShares) -> List[object]:
+        """Pipelined: host decode + HPKE of job k + 1 overlaps the GPU preparation of job k.
+
+        Entry k is job k's AggregationJobResp bytes, or the Prio3GpuError that failed that request
+        alone (InvalidMessage: duplicate report IDs or a non-empty aggregation parameter;
+        EmptyAggregation): Janus answers such a request with an error and the other jobs carry
+        on (aggregator.rs:1588-1605, :1851-1863).  An engine failure while preparing a job ends
+        the stream (re-raised), after the staging buffer of the job opened ahead is released."""
+        out: List[object] = []
         if not reqs:
             return out
         with ThreadPoolExecutor(max_workers=1) as pool:
             nxt = pool.submit(self.open, reqs[0])
             for k in range(len(reqs)):
-                cur = nxt.result()
+                try:
+                    cur = nxt.result()
+                except Prio3GpuError as e:  # this request alone is rejected
+                    cur = e
                 if k + 1 < len(reqs):
                     nxt = pool.submit(self.open, reqs[k + 1])
-                out.append(self.prepare(cur, agg))
+                if isinstance(cur, Prio3GpuError):
+                    out.append(cur)
+                    continue
+                try:
+                    out.append(self.prepare(cur, agg))
+                except BaseException:
+                    if k + 1 < len(reqs):  # drain the job opened ahead and free its buffer
+                        try:
+                            ahead = nxt.result()
+                        except BaseException:
+                            ahead = None
+                        if isinstance(ahead, _Opened):
+                            self._pinned.release(ahead.buf)
+                    raise
         return out
 
     def close(self):

@@ -36,7 +36,7 @@ from typing import Callable, List, Optional, Sequence
 import numpy as np
 
 from . import codec as C
-from ._lib import EmptyAggregation
+from ._lib import EmptyAggregation, Prio3GpuError
 from .prio3 import AggregateShares, PrepareState, Prio3Gpu
 
 REPORT_DROPPED, VDAF_PREP_ERROR, INVALID_MESSAGE = 2, 5, 8
@@ -232,27 +232,60 @@ class LeaderAggregateInit:
         return self.finish(st, send(st.request), agg)
 
     def run_jobs(self, jobs: Sequence[LeaderJob], send: Callable[[bytes], bytes],
-                 agg: AggregateShares, stats: Optional[list] = None) -> List[np.ndarray]:
+                 agg: AggregateShares, stats: Optional[list] = None) -> List[object]:
         """Pipelined over jobs: H2D of job k+1 || GPU prepare_init of job k; helper round trip
-        of job k || GPU work of job k+1.  `stats`, if given, receives each job's stage times."""
-        out: List[np.ndarray] = []
+        of job k || GPU work of job k+1.  `stats`, if given, receives each job's stage times.
+
+        Entry k is job k's per-report final statuses, or the exception that failed job k alone:
+        an empty job (EmptyAggregation), a response that does not answer the sent reports
+        (Prio3GpuError, aggregation_job_driver.rs:556-573), a failed helper round trip.  Janus
+        steps each aggregation job on its own (job_driver.rs:119-216), so a failing job never
+        strands the one in flight: the request already sent for job k-1 is still finished, so
+        the leader's aggregate keeps the reports the helper has accumulated."""
+        out: List[object] = [None] * len(jobs)
         if not jobs:
             return out
         with ThreadPoolExecutor(max_workers=1) as h2d, ThreadPoolExecutor(max_workers=1) as net:
             staged = h2d.submit(self.stage, jobs[0])
-            inflight = None
-            for k in range(len(jobs)):
-                d_in = staged.result()
-                if k + 1 < len(jobs):
-                    staged = h2d.submit(self.stage, jobs[k + 1])
-                st = self.init(jobs[k], d_in)
-                fut = net.submit(send, st.request)
-                if inflight is not None:
-                    out.append(self.finish(inflight[0], inflight[1].result(), agg))
-                    if stats is not None:
-                        stats.append(inflight[0].times_ms)
-                inflight = (st, fut)
-            out.append(self.finish(inflight[0], inflight[1].result(), agg))
-            if stats is not None:
-                stats.append(inflight[0].times_ms)
+            inflight = None  # (job index, LeaderStepped, response future)
+
+            def finish_inflight():
+                k0, st0, fut0 = inflight
+                try:
+                    resp = fut0.result()
+                except Exception as e:  # the helper round trip failed: this job alone
+                    self._release(st0.state)
+                    st0.d_in = None
+                    out[k0] = e
+                    return
+                try:
+                    out[k0] = self.finish(st0, resp, agg)
+                except Prio3GpuError as e:
+                    out[k0] = e
+                if stats is not None:
+                    stats.append(st0.times_ms)
+
+            try:
+                for k in range(len(jobs)):
+                    try:
+                        d_in = staged.result()
+                    except Exception as e:
+                        d_in = e
+                    if k + 1 < len(jobs):
+                        staged = h2d.submit(self.stage, jobs[k + 1])
+                    started = None
+                    if isinstance(d_in, Exception):
+                        out[k] = d_in
+                    else:
+                        try:
+                            st = self.init(jobs[k], d_in)
+                            started = (k, st, net.submit(send, st.request))
+                        except Prio3GpuError as e:  # EmptyAggregation, a rejected batch
+                            out[k] = e
+                    if inflight is not None:
+                        finish_inflight()
+                    inflight = started
+            finally:
+                if inflight is not None:  # also on abort: never leave a sent job unfinished
+                    finish_inflight()
         return out

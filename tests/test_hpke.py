@@ -256,3 +256,52 @@ def test_open_report_shares_one_key_batch_matches_single_opens():
             continue
         assert st[i] == 0, i
         assert pts[int(offs[i]):int(offs[i + 1])].tobytes()[6:] == payloads[i]
+
+
+@pytest.mark.gpu
+def test_pipelined_helper_driver_isolates_bad_requests():
+    """handle_jobs with a duplicate-report-ID request and an empty request between valid ones:
+    those entries are InvalidMessage / EmptyAggregation, the other jobs are answered and
+    accumulated, and no staging buffer stays busy (one bad request must not abort
+    the stream or leak the buffer of the job opened ahead)."""
+    from janus_amd._lib import EmptyAggregation, InvalidMessage
+    from janus_amd.helper import HelperAggregateInit
+    from janus_amd.prio3 import Prio3Gpu
+    from tests.reports import CONFIGS, expected_aggregate, make_batch
+    name = "sum8"
+    b = make_batch(name, 16)
+    c = CONFIGS[name]
+    v = Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"], length=c["length"],
+                 chunk_length=c["chunk"])
+    task_id = os.urandom(32)
+    tk = H.generate_hpke_config_and_private_key(3)
+    info = H.application_info(H.Label.INPUT_SHARE, H.ROLE_CLIENT, H.ROLE_HELPER)
+    times = list(range(1000, 1000 + b.n))
+    cts = []
+    for r in range(b.n):
+        pt = b"\x00\x00" + len(b.helper_in[r]).to_bytes(4, "big") + b.helper_in[r].tobytes()
+        aad = H.input_share_aad(task_id, b.nonces[r].tobytes(), times[r], b.public[r].tobytes())
+        cts.append(H.seal(tk.config, info, pt, aad))
+
+    def req(idx):
+        return C.encode_agg_init_req(C.TIME_INTERVAL, None, b"", b.nonces[idx],
+                                     [times[i] for i in idx], b.public[idx],
+                                     [cts[i] for i in idx], b.leader_prep[idx])
+
+    a, d = list(range(0, 8)), list(range(8, 16))
+    dup = [0, 1, 2, 1]
+    empty = C.encode_agg_init_req(C.TIME_INTERVAL, None, b"", np.zeros((0, 16), np.uint8), [],
+                                  np.zeros((0, b.public.shape[1]), np.uint8), [],
+                                  np.zeros((0, b.leader_prep.shape[1]), np.uint8))
+    drv = HelperAggregateInit(v, task_id, [tk], hpke_threads=2)
+    hagg = v.new_aggregate(1)
+    out = drv.handle_jobs([req(a), req(dup), empty, req(d)], hagg)
+    assert isinstance(out[1], InvalidMessage) and isinstance(out[2], EmptyAggregation)
+    for idx, resp in ((a, out[0]), (d, out[3])):
+        _, st = C.gather_helper_resps(v.sizes, resp, b.nonces[idx], np.zeros(len(idx), np.uint8))
+        assert (st == 0).all()
+    got, cnt = hagg.read(0)
+    exp, ecnt = expected_aggregate(b, "helper")
+    assert got == exp and cnt == ecnt == b.n
+    assert not any(drv._pinned._busy)
+    drv.close()

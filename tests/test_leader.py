@@ -166,3 +166,52 @@ def test_leader_driver_rejects_mismatched_response():
     good = C.encode_agg_job_resp(b.nonces, b.prep_msg, 16, np.zeros(b.n, np.uint8))
     st = drv.handle(job, lambda req: good, lagg)
     assert (st == 0).all() and lagg.read(0)[1] == b.n
+
+
+@pytest.mark.gpu
+def test_leader_run_jobs_isolates_failing_jobs():
+    """run_jobs with an empty job and a job whose helper answers the wrong reports between valid
+    ones: those two entries are the jobs' errors, the job in flight before each failure is still
+    finished (its request already reached the helper, which accumulated it), and the leader's
+    aggregate covers exactly the finished jobs (a failing init must not strand job
+    k-1)."""
+    from janus_amd._lib import EmptyAggregation, Prio3GpuError
+    from janus_amd.helper import HelperAggregateInit
+    from janus_amd.leader import LeaderAggregateInit
+    from tests.reports import expected_aggregate
+    b, mk, task_id, tk, times, cts, LeaderJob = _leader_setup("sum8", 24)
+    lv, hv = mk(), mk()
+    drv = LeaderAggregateInit(lv)
+
+    def job(j):
+        ids, eb, eo, pb, po = LeaderJob.pack_ciphertexts(cts[j])
+        return LeaderJob(b.nonces[j], times[j], b.public[j], b.leader_in[j], ids, eb, eo, pb, po)
+
+    e = slice(0, 0)
+    jobs = [job(slice(0, 8)), job(e), job(slice(8, 16)), job(slice(16, 24))]
+    helper = HelperAggregateInit(hv, task_id, [tk], hpke_threads=2)
+    hagg, lagg = hv.new_aggregate(1), lv.new_aggregate(1)
+    calls = []
+
+    def send(req):
+        calls.append(len(calls))
+        resp = helper.handle(req, hagg)
+        if len(calls) == 3:  # the fourth job's helper answers only its first report
+            return C.encode_agg_job_resp(b.nonces[16:17], b.prep_msg[16:17], 16,
+                                         np.zeros(1, np.uint8))
+        return resp
+
+    out = drv.run_jobs(jobs, send, lagg)
+    assert isinstance(out[1], EmptyAggregation)
+    assert isinstance(out[3], Prio3GpuError)
+    assert (out[0] == 0).all() and (out[2] == 0).all()
+    mask = np.zeros(b.n, bool)
+    mask[:16] = True
+    got, cnt = lagg.read(0)
+    want, wcnt = expected_aggregate(b, "leader", mask=mask)
+    assert got == want and cnt == wcnt == 16
+    # the driver keeps working after the failures
+    st = drv.handle(job(slice(0, 8)), lambda req: helper.handle(req, hagg), lagg)
+    assert (st == 0).all() and lagg.read(0)[1] == 24
+    helper.close()
+    drv.close()
