@@ -285,6 +285,15 @@ const char* prio3gpu_prof_kernel_name(int kernel_id);
  * (as PRIO3GPU_EXACT_SQUEEZE=1 does in the real kernels).  Runs on the current HIP device. */
 int prio3gpu_test_squeeze(int field_size, const uint64_t* blocks, size_t nblocks, uint32_t n,
                           uint8_t* out, int exact);
+/* TEST ONLY.  The FLP-query phase of prepare_init (agg_id 0) over caller-supplied randomness
+ * instead of the XOF's: leader_input_shares n x leader_input_share, query_rand n x qr_len x
+ * field_size (qr_len = 1, 2 for FixedPoint), joint_rand n x joint_rand_len x field_size, own_parts
+ * n x 16 (the prep share's joint-rand part).  Writes the prep shares; a query point that is a root
+ * of unity sets status 5 (VdafPrepError), as prio does.  Lets tests reach the branches that
+ * SHAKE128 output reaches with negligible probability (t^m == 1, r^m == 1). */
+int prio3gpu_test_flp_query(prio3gpu_ctx* ctx, size_t n, const uint8_t* leader_input_shares,
+                            const uint8_t* query_rand, const uint8_t* joint_rand,
+                            const uint8_t* own_parts, uint8_t* out_prep_shares, uint8_t* status);
 
 /* Device memory helpers (bench / tests that stage inputs in HBM without torch). */
 int prio3gpu_dev_alloc(prio3gpu_ctx* ctx, size_t bytes, void** out);

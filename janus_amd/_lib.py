@@ -134,6 +134,7 @@ def _declare(lib):
         "prio3gpu_prof_read": (c.c_int, [P, P, P, c.c_int]),
         "prio3gpu_prof_kernel_name": (c.c_char_p, [c.c_int]),
         "prio3gpu_test_squeeze": (c.c_int, [c.c_int, P, c.c_size_t, c.c_uint32, u8p, c.c_int]),
+        "prio3gpu_test_flp_query": (c.c_int, [P, c.c_size_t, u8p, u8p, u8p, u8p, u8p, u8p]),
         "prio3gpu_dev_alloc": (c.c_int, [P, c.c_size_t, c.POINTER(P)]),
         "prio3gpu_dev_free": (c.c_int, [P, P]),
         "prio3gpu_memcpy": (c.c_int, [P, P, P, c.c_size_t]),
@@ -195,7 +196,7 @@ EXPORTED = [
     "prio3gpu_prepare_shares_to_prepare_message", "prio3gpu_prepare_next", "prio3gpu_helper_init",
     "prio3gpu_random_size", "prio3gpu_shard", "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
     "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
-    "prio3gpu_prof_kernel_name", "prio3gpu_test_squeeze", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
+    "prio3gpu_prof_kernel_name", "prio3gpu_test_squeeze", "prio3gpu_test_flp_query", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
     "prio3gpu_last_error", "prio3gpu_build_hash", "prio3gpu_unshard", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
     "prio3gpu_apply_faults", "prio3gpu_check_agg_init_req", "prio3gpu_batch_aggregation_merge",
     "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",

@@ -2004,6 +2004,60 @@ int prio3gpu_test_squeeze(int field_size, const uint64_t* blocks, size_t nblocks
   return rc;
 }
 
+// Test-only: the FLP query phase of prepare_init over caller-supplied randomness.  Real query and
+// joint randomness come out of SHAKE128, so the branches for a query point that is a root of unity
+// (prio's "invalid query randomness", a VdafPrepError) and for a joint-rand element r with
+// r^m == 1 (the closed-form gadget sum's degenerate case in k_flp_query_lane) are unreachable
+// with real inputs; this entry runs launch_prep_query on crafted values so tests can compare them
+// with the oracle's direct flp_query.
+int prio3gpu_test_flp_query(prio3gpu_ctx* c, size_t n, const uint8_t* leader_input_shares,
+                            const uint8_t* query_rand, const uint8_t* joint_rand,
+                            const uint8_t* own_parts, uint8_t* out_prep_shares, uint8_t* status) {
+  if (!c || !leader_input_shares || !query_rand || !own_parts || !status || n == 0 ||
+      (c->cfg.jr_len && !joint_rand)) {
+    set_err("test_flp_query: bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const Cfg& g = c->cfg;
+  prio3gpu_state* st = nullptr;
+  CHK(prio3gpu_state_create(c, 0, n, &st));
+  int rc = 0;
+  auto run = [&]() -> int {
+    const size_t qr = (size_t)g.qr_len * g.es;
+    CHK(st->input.ensure(n * g.leader_share_len));
+    HIPCHK(hipMemcpyAsync(st->input.p, leader_input_shares, n * g.leader_share_len,
+                          hipMemcpyDefault, c->stream));
+    // query randomness rows have a 16-byte slot per element (k_query_rand's layout)
+    std::vector<uint8_t> t(n * 16 * g.qr_len, 0);
+    for (size_t r = 0; r < n; ++r)
+      for (uint32_t i = 0; i < g.qr_len; ++i)
+        memcpy(&t[r * 16 * g.qr_len + (size_t)i * g.es], query_rand + r * qr + (size_t)i * g.es,
+               g.es);
+    HIPCHK(hipMemcpyAsync(st->t.p, t.data(), t.size(), hipMemcpyHostToDevice, c->stream));
+    if (g.jr_len)
+      HIPCHK(hipMemcpyAsync(st->jr.p, joint_rand, n * (size_t)g.jr_len * g.es, hipMemcpyDefault,
+                            c->stream));
+    HIPCHK(hipMemcpyAsync(st->part.p, own_parts, n * 16, hipMemcpyDefault, c->stream));
+    HIPCHK(hipMemcpyAsync(st->status.p, status, n, hipMemcpyDefault, c->stream));
+    st->meas_rows = CRows{st->input.u8(), g.leader_share_len};
+    st->proof_rows = CRows{st->input.u8() + (size_t)g.meas_len * g.es, g.leader_share_len};
+    st->n = n;
+    st->xof_done = true;
+    if (is_f64(c))
+      CHK(launch_prep_query<Field64Ops>(c, st, n, st->status.u8()));
+    else
+      CHK(launch_prep_query<Field128Ops>(c, st, n, st->status.u8()));
+    CHK(copy_out(c, out_prep_shares, st->prep.p, n * g.prep_share_len));
+    CHK(copy_out(c, status, st->status.p, n));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+  };
+  rc = run();
+  prio3gpu_state_destroy(st);
+  return rc;
+}
+
 int prio3gpu_prof_enable(prio3gpu_ctx* c, int on) {
   if (!c) {
     set_err("null context");

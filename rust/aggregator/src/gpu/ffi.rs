@@ -222,6 +222,10 @@ extern "C" {
     pub fn prio3gpu_prof_kernel_name(kernel_id: c_int) -> *const c_char;
     pub fn prio3gpu_test_squeeze(field_size: c_int, blocks: *const u64, nblocks: usize, n: u32,
                                  out: *mut u8, exact: c_int) -> c_int;
+    pub fn prio3gpu_test_flp_query(ctx: *mut prio3gpu_ctx, n: usize,
+                                   leader_input_shares: *const u8, query_rand: *const u8,
+                                   joint_rand: *const u8, own_parts: *const u8,
+                                   out_prep_shares: *mut u8, status: *mut u8) -> c_int;
     pub fn prio3gpu_dev_alloc(ctx: *mut prio3gpu_ctx, bytes: usize, out: *mut *mut c_void)
                               -> c_int;
     pub fn prio3gpu_dev_free(ctx: *mut prio3gpu_ctx, p: *mut c_void) -> c_int;

@@ -87,3 +87,98 @@ def test_query_phase_without_xof_phase_is_an_error():
     out = np.zeros((4, v.sizes.prep_share), np.uint8)
     v.prepare_init_query(st, out, status)
     assert (status == 0).all() and (out == b.leader_prep).all()
+
+
+def test_stale_mark_is_rejected_and_ctx_wait_takes_no_mark():
+    """Marks carry a generation: a mark re-recorded by 16 newer ones is refused
+    instead of silently waiting on newer work, and prio3gpu_ctx_wait records a private event, so
+    it never consumes the other context's mark ring."""
+    from janus_amd.prio3 import Prio3Gpu, Prio3GpuError
+    from tests.reports import CONFIGS, make_batch
+    b = make_batch("sum8", 4)
+    c = CONFIGS["sum8"]
+    A = Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"])
+    B = Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"])
+    m = A.mark()
+    for _ in range(40):
+        B.wait_for(A)  # no marks taken on A
+    B.wait_for(A, m)   # still valid
+    for _ in range(16):
+        A.mark()
+    with pytest.raises(Prio3GpuError, match="stale mark"):
+        B.wait_for(A, m)
+    B.wait_for(A, A.mark())
+    with pytest.raises(Prio3GpuError):
+        B.wait_for(A, 3)  # never a mark (generation 0)
+    A.sync()
+    B.sync()
+
+
+@pytest.mark.parametrize("with_total", [True, False])
+def test_rccl_flush_is_stream_ordered_in_async_mode(with_total):
+    """prio3gpu_agg_allreduce queues like every other all-device call: two jobs
+    accumulated and flushed back to back on an async context with no host wait in between give
+    the same aggregate, count, checksum and interval as the host-side
+    BatchAggregation::merged_with of the two jobs' partials (prio3gpu_batch_aggregation_merge)."""
+    import torch
+    from janus_amd._lib import check, lib
+    from janus_amd.prio3 import Comm, Prio3Gpu
+    from tests.reports import CONFIGS, expected_aggregate, make_batch
+    name = "sumvec_small"
+    b = make_batch(name, 24)
+    c = CONFIGS[name]
+    v = Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"], length=c["length"],
+                 chunk_length=c["chunk"])
+    s = v.sizes
+    dev = torch.device("cuda", 0)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    nz, pub, lin, msgs = d(b.nonces), d(b.public), d(b.leader_in), d(b.prep_msg)
+    times = torch.arange(b.n, dtype=torch.int64, device=dev) + 7000
+    lst = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    P = lambda t: t.data_ptr()
+    jobs = [slice(0, 10), slice(10, 24)]
+    states = [v.new_state(0, 14) for _ in jobs]
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    local = v.new_aggregate(1)
+    total = v.new_aggregate(1) if with_total else None
+    torch.cuda.synchronize()
+    v.set_async(True)
+    for st, j in zip(states, jobs):
+        n = j.stop - j.start
+        check(lib().prio3gpu_prepare_init(v._ctx, st._h, n, P(nz[j]), P(pub[j]), P(lin[j]), None,
+                                          P(lst[j])), "prepare_init")
+        check(lib().prio3gpu_prepare_next(v._ctx, st._h, n, P(msgs[j]), P(lst[j]), None, None,
+                                          local._h), "prepare_next")
+        check(lib().prio3gpu_agg_update_reports(local._h, n, P(nz[j]), P(times[j]), P(lst[j]),
+                                                None), "report meta")
+        comm.allreduce(v, local, total)  # queued: no host wait
+    v.sync()
+    v.set_async(False)
+    assert int(lst.max()) == 0
+    got = (total if with_total else local).read(0)
+    want = expected_aggregate(b, "leader")
+    assert got[0] == want[0] and got[1] == want[1] == b.n
+    ck, iv = (total if with_total else local).read_reports(0)
+    import hashlib
+    exp_ck = bytes(32)
+    for i in range(b.n):
+        exp_ck = bytes(x ^ y for x, y in zip(exp_ck, hashlib.sha256(b.nonces[i].tobytes()).digest()))
+    assert ck == exp_ck and iv == (7000, b.n)
+    # the same through the host merge of the two jobs' partials
+    parts = []
+    for j in jobs:
+        m = np.zeros(b.n, bool)
+        m[j] = True
+        sh, cnt = expected_aggregate(b, "leader", mask=m)
+        pck = bytes(32)
+        for i in np.flatnonzero(m):
+            pck = bytes(x ^ y for x, y in zip(pck, hashlib.sha256(b.nonces[i].tobytes()).digest()))
+        parts.append((sh, cnt, pck, 7000 + j.start, j.stop - j.start))
+    from janus_amd.parallel import BatchAggregation, merge_batch_aggregations
+    merged = merge_batch_aggregations(s.field_size, [BatchAggregation(sh, cnt, pck, (t0, dur))
+                                                     for sh, cnt, pck, t0, dur in parts])
+    assert (merged.aggregate_share, merged.report_count, merged.checksum, merged.interval) == \
+        (got[0], got[1], ck, iv)
+    if with_total:
+        assert local.read(0)[1] == 0 and local.read_reports(0) == (bytes(32), (0, 0))
+    comm.close()
