@@ -227,6 +227,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sumvec", choices=list(CONFIGS))
     ap.add_argument("--reports", type=int, default=0, help="reports per GPU per step (B)")
+    ap.add_argument("--leader-pitch", type=int, default=0,
+                    help="row pitch of the leader input shares in HBM (0 packed, -1 next 128 B)")
     ap.add_argument("--unique", type=int, default=0, help="CPU-baseline sample size (reports)")
     ap.add_argument("--gen-threads", type=int, default=16)
     ap.add_argument("--cpu-baseline", type=int, default=1)
@@ -317,11 +319,29 @@ def main():
     d_rand = torch.from_numpy(syn["rand"]).to(dev)
     d_pub = torch.empty((B, s.public_share), dtype=torch.uint8, device=dev) if s.public_share \
         else None
-    d_lin = torch.empty((B, s.leader_input_share), dtype=torch.uint8, device=dev)
+    # leader input shares at a row pitch (--leader-pitch; 0 = packed wire rows): what a Janus
+    # caller decoding LeaderStoredReports into 128-B-aligned rows hands prio3gpu_prepare_init
+    lpitch = args.leader_pitch if args.leader_pitch > 0 else s.leader_input_share
+    if args.leader_pitch < 0:  # auto: the next multiple of 128 B
+        lpitch = (s.leader_input_share + 127) // 128 * 128
+    assert lpitch >= s.leader_input_share and lpitch % 16 == 0, "bad --leader-pitch"
+    d_lin_rows = torch.empty((B, lpitch), dtype=torch.uint8, device=dev)
+    d_lin = d_lin_rows[:, :s.leader_input_share]
     d_hin = torch.empty((B, s.helper_input_share), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    hs0 = vdaf.new_state(1, B)
-    vdaf.shard(hs0, d_nonces, d_meas, d_rand, out=(d_pub, d_lin, d_hin))
+    SC = B if lpitch == s.leader_input_share else min(B, 32768)  # shard chunk (packed: one call)
+    hs0 = vdaf.new_state(1, SC)
+    d_tmp = d_lin if SC == B else torch.empty((SC, s.leader_input_share), dtype=torch.uint8,
+                                                device=dev)
+    for c0 in range(0, B, SC):
+        c1 = min(B, c0 + SC)
+        vdaf.shard(hs0, d_nonces[c0:c1], d_meas[c0:c1], d_rand[c0:c1],
+                   out=(d_pub[c0:c1] if d_pub is not None else None, d_tmp[:c1 - c0],
+                        d_hin[c0:c1]))
+        if SC != B:  # torch's stream; the next shard (engine stream) reuses d_tmp
+            d_lin[c0:c1].copy_(d_tmp[:c1 - c0])
+            torch.cuda.synchronize()
+    del d_tmp
     hs0.close()
     del d_rand
     gen_s = time.time() - t0
@@ -371,6 +391,7 @@ def main():
         wk.hv = (Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk,
                           device=gpu, xof=xof_id) if args.overlap else wk.v)
         wk.ls, wk.hs = wk.v.new_state(0, wk.n), wk.hv.new_state(1, wk.n)
+        wk.ls.set_input_pitch(0 if lpitch == s.leader_input_share else lpitch)
         wk.lagg, wk.hagg = wk.v.new_aggregate(1), wk.hv.new_aggregate(1)
         wk.lpart, wk.hpart = ((wk.v.new_aggregate(1), wk.hv.new_aggregate(1)) if rccl
                               else (wk.lagg, wk.hagg))
@@ -438,7 +459,9 @@ def main():
         A, Bv = wk.v, wk.hv
         A.set_async(True)
         Bv.set_async(True)
-        pipe = dict(ls=[wk.ls, wk.v.new_state(0, wk.n)],
+        ls2 = wk.v.new_state(0, wk.n)
+        ls2.set_input_pitch(0 if lpitch == s.leader_input_share else lpitch)
+        pipe = dict(ls=[wk.ls, ls2],
                     lst=[d_lst, torch.zeros(B, dtype=torch.uint8, device=dev)])
 
     def run_pipelined(k_steps):

@@ -149,6 +149,13 @@ void* prio3gpu_ctx_stream(prio3gpu_ctx* ctx);
  * (Prio3PrepareState for a whole batch). */
 int prio3gpu_state_create(prio3gpu_ctx* ctx, int agg_id, size_t capacity, prio3gpu_state** out);
 int prio3gpu_state_destroy(prio3gpu_state* st);
+/* Row pitch of the input shares this state's prepare_init / prepare_init_xof / helper_init calls
+ * read: report i's input share at input_shares + i * pitch (0 = packed, the default: pitch = the
+ * input share length).  A non-zero pitch is a multiple of 16 and >= the share length.  A caller
+ * that decodes leader input shares (134,944 B for SumVec(8,1000)) into 128-B-aligned rows
+ * (pitch 135,040) gives k_jr's LDS-DMA windows and the FLP wire pass line-aligned rows
+ * (aggregator_core/src/datastore.rs:1298-1304 decodes each LeaderStoredReport's share). */
+int prio3gpu_state_set_input_pitch(prio3gpu_state* st, size_t pitch);
 
 /* Aggregate shares: `num_slots` batch identifiers (caller maps BatchIdentifier -> slot). */
 int prio3gpu_agg_create(prio3gpu_ctx* ctx, uint32_t num_slots, prio3gpu_agg** out);

@@ -112,6 +112,7 @@ def _declare(lib):
         "prio3gpu_ctx_stream": (P, [P]),
         "prio3gpu_state_create": (c.c_int, [P, c.c_int, c.c_size_t, c.POINTER(P)]),
         "prio3gpu_state_destroy": (c.c_int, [P]),
+        "prio3gpu_state_set_input_pitch": (c.c_int, [P, c.c_size_t]),
         "prio3gpu_agg_create": (c.c_int, [P, c.c_uint32, c.POINTER(P)]),
         "prio3gpu_agg_destroy": (c.c_int, [P]),
         "prio3gpu_agg_reset": (c.c_int, [P]),
@@ -190,6 +191,7 @@ EXPORTED = [
     "prio3gpu_ctx_wait_mark",
     "prio3gpu_prepare_init_xof", "prio3gpu_prepare_init_query",
     "prio3gpu_ctx_stream", "prio3gpu_state_create", "prio3gpu_state_destroy",
+    "prio3gpu_state_set_input_pitch",
     "prio3gpu_agg_create", "prio3gpu_agg_destroy", "prio3gpu_agg_reset", "prio3gpu_agg_read",
     "prio3gpu_agg_merge_bytes", "prio3gpu_agg_update_reports", "prio3gpu_agg_read_reports",
     "prio3gpu_prepare_init",

@@ -251,6 +251,7 @@ struct prio3gpu_state {
   int agg_id = 0;
   size_t cap = 0;
   size_t n = 0;
+  size_t in_pitch = 0;  // row pitch of the caller's input shares (0: packed, the share length)
   DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input, w;
   DevBuf fpart, flags;  // FixedPointBoundedL2VecSum: wire partials per row group, query flags
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
@@ -577,6 +578,12 @@ int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, 
 template <class FO>
 int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_status);
 
+// Row pitch of a state's input shares: the caller's (prio3gpu_state_set_input_pitch) or packed.
+size_t input_pitch(const prio3gpu_state* st) {
+  const Cfg& g = st->ctx->cfg;
+  return st->in_pitch ? st->in_pitch : (st->agg_id == 0 ? g.leader_share_len : g.helper_share_len);
+}
+
 // prepare_init, first phase: query randomness, (helper) share expansion, joint randomness.
 template <class FO>
 int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_nonces,
@@ -613,10 +620,11 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     st->spec_e1 = se1;
   }
   CRows meas, proof, blinds;
+  const size_t in_pitch = input_pitch(st);
   if (st->agg_id == 0) {
-    meas = CRows{d_in, g.leader_share_len};
-    proof = CRows{d_in + (size_t)g.meas_len * es, g.leader_share_len};
-    blinds = CRows{d_in + (size_t)(g.meas_len + g.proof_len) * es, g.leader_share_len};
+    meas = CRows{d_in, in_pitch};
+    proof = CRows{d_in + (size_t)g.meas_len * es, in_pitch};
+    blinds = CRows{d_in + (size_t)(g.meas_len + g.proof_len) * es, in_pitch};
   } else {
     Rows mo{st->meas.u8(), (size_t)g.meas_len * es};
     Rows po{st->proof.u8(), (size_t)g.proof_len * es};
@@ -636,7 +644,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
                              c->hx_lds ? std::min<size_t>(c->hx_lds, kSpreadLds)
                                        : (spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0),
                              c->stream, g, N,
-                             CRows{d_in, g.helper_share_len}, nonces, pub, mo, po,
+                             CRows{d_in, in_pitch}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
                              Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb,
                              c->hx_spec ? spec_lo : nullptr, spec_cy);
@@ -658,11 +666,11 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     {
       PROF(KID_EXPAND);
       hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
-                         (uint32_t)st->agg_id, CRows{d_in, g.helper_share_len}, mo, po, d_status);
+                         (uint32_t)st->agg_id, CRows{d_in, in_pitch}, mo, po, d_status);
     }
     meas = CRows{mo.base, mo.stride};
     proof = CRows{po.base, po.stride};
-    blinds = CRows{d_in + 32, g.helper_share_len};
+    blinds = CRows{d_in + 32, in_pitch};
   }
   bool ring_done = false;
   if constexpr (FO::ES == 16) {
@@ -1229,6 +1237,22 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   return 0;
 }
 
+int prio3gpu_state_set_input_pitch(prio3gpu_state* st, size_t pitch) {
+  if (!st) {
+    set_err("null state");
+    return PRIO3GPU_E_ARG;
+  }
+  const Cfg& g = st->ctx->cfg;
+  const size_t len = st->agg_id == 0 ? g.leader_share_len : g.helper_share_len;
+  if (pitch != 0 && (pitch < len || pitch % 16 != 0)) {
+    set_err("input pitch %zu: must be 0 or a multiple of 16 that is >= the input share (%zu B)",
+            pitch, len);
+    return PRIO3GPU_E_ARG;
+  }
+  st->in_pitch = pitch;
+  return 0;
+}
+
 int prio3gpu_state_destroy(prio3gpu_state* st) {
   if (!st) return 0;
   if (st->ctx) (void)hipStreamSynchronize(st->ctx->stream);
@@ -1451,7 +1475,7 @@ int prio3gpu_prepare_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const u
   CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));
   CHK(stage_in(c, st->pub, public_shares, n * g.public_share_len, &d_pub));
   const size_t in_len = st->agg_id == 0 ? g.leader_share_len : g.helper_share_len;
-  CHK(stage_in(c, st->input, input_shares, n * in_len, &d_in));
+  CHK(stage_in(c, st->input, input_shares, (n - 1) * input_pitch(st) + in_len, &d_in));
   uint8_t* d_status;
   CHK(stage_status(c, st->status, status, n, &d_status));
   if (is_f64(c))
@@ -1478,7 +1502,7 @@ int prio3gpu_prepare_init_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, con
   CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));
   CHK(stage_in(c, st->pub, public_shares, n * g.public_share_len, &d_pub));
   const size_t in_len = st->agg_id == 0 ? g.leader_share_len : g.helper_share_len;
-  CHK(stage_in(c, st->input, input_shares, n * in_len, &d_in));
+  CHK(stage_in(c, st->input, input_shares, (n - 1) * input_pitch(st) + in_len, &d_in));
   uint8_t* d_status;
   CHK(stage_status(c, st->status, status, n, &d_status));
   if (is_f64(c))
@@ -1671,7 +1695,8 @@ int prio3gpu_helper_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const ui
   const uint8_t *d_nonces, *d_pub, *d_in, *d_lps;
   CHK(stage_in(c, st->nonces, nonces, n * 16, &d_nonces));
   CHK(stage_in(c, st->pub, public_shares, n * g.public_share_len, &d_pub));
-  CHK(stage_in(c, st->input, helper_input_shares, n * g.helper_share_len, &d_in));
+  CHK(stage_in(c, st->input, helper_input_shares, (n - 1) * input_pitch(st) + g.helper_share_len,
+               &d_in));
   CHK(stage_in(c, c->io[0], leader_prep_shares, n * g.prep_share_len, &d_lps));
   uint8_t* d_status;
   CHK(stage_status(c, st->status, status, n, &d_status));

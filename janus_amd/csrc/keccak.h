@@ -160,51 +160,6 @@ DEVI void keccak_x(uint64_t a[25], const Xof& x) {
   for (int i = 0; i < 25; ++i) a[i] = ((uint64_t)h[i] << 32) | l[i];
 }
 
-// keccak_x with a hook between rounds: `hook.template after<R>()` runs after round R for
-// R = 12..23 (the rounds both XOFs execute), so a sponge loop can spread its per-block memory
-// instructions (stores of the previous block, LDS-DMA fills of the next one) across the
-// permutation instead of issuing them as one burst the wave waits behind.
-// All 50 state words through empty volatile asm with a memory clobber: the rounds after a hook
-// cannot be hoisted above the hook's memory instructions, nor the hook's instructions above the
-// rounds before it (asm volatile / memory operations keep their order; the state words carry the
-// data dependency).
-DEVI void keccak_fence(uint32_t l[25], uint32_t h[25]) {
-#define P3G_F5(a, i) "+v"(a[i]), "+v"(a[i + 1]), "+v"(a[i + 2]), "+v"(a[i + 3]), "+v"(a[i + 4])
-  asm volatile("" : P3G_F5(l, 0), P3G_F5(l, 5) : : "memory");
-  asm volatile("" : P3G_F5(l, 10), P3G_F5(l, 15) : : "memory");
-  asm volatile("" : P3G_F5(l, 20), P3G_F5(h, 0) : : "memory");
-  asm volatile("" : P3G_F5(h, 5), P3G_F5(h, 10) : : "memory");
-  asm volatile("" : P3G_F5(h, 15), P3G_F5(h, 20) : : "memory");
-#undef P3G_F5
-}
-
-template <int R, int END, class H>
-DEVI void keccak_rounds32_h(uint32_t l[25], uint32_t h[25], H& hook) {
-  if constexpr (R < END) {
-    keccak_round32<R>(l, h);
-    if constexpr (H::template active<R>()) {
-      keccak_fence(l, h);
-      hook.template after<R>();
-      keccak_fence(l, h);
-    }
-    keccak_rounds32_h<R + 1, END>(l, h, hook);
-  }
-}
-
-template <class H>
-DEVI void keccak_x_h(uint64_t a[25], const Xof& x, H& hook) {
-  uint32_t l[25], h[25];
-#pragma unroll
-  for (int i = 0; i < 25; ++i) {
-    l[i] = (uint32_t)a[i];
-    h[i] = (uint32_t)(a[i] >> 32);
-  }
-  if (x.full) keccak_rounds32<0, 12>(l, h);
-  keccak_rounds32_h<12, 24>(l, h, hook);
-#pragma unroll
-  for (int i = 0; i < 25; ++i) a[i] = ((uint64_t)h[i] << 32) | l[i];
-}
-
 // ------------------------------------------------------------------------------------------------
 // XofShake128 message framing (prio src/vdaf/xof.rs; VDAF-07 §6.2.1):
 //   SHAKE128( u8(8) || dst[8] || seed[16] || binder )       rate 168 B = 21 words, pad 0x1F..0x80

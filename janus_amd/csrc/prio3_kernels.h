@@ -102,29 +102,19 @@ struct SqueezeVec;
 // exact per-element path (prio's rejection sampling), so the output is the same either way.
 DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 
-// A fast block's element stores, deferred into the next permutation: the Keccak hook issues store
-// k after round 12 + k, so the block's 10-11 per-lane-row stores (64 rows per wave-instruction)
-// reach the memory pipeline spread over the permutation rather than as one burst the wave waits
-// behind (k_expand, PRIO3GPU build flag P3G_EXPAND_DEFER).
-struct PendingStores {
-  ulonglong2 v[11];
-  ulonglong2* base = nullptr;
-  uint32_t cnt = 0;  // 0, 10 or 11 pending elements
-  template <int R>
-  static constexpr bool active() { return R >= 12 && R < 23; }
-  template <int R>
-  DEVI void after() {  // store k = R - 12, between the rounds (keccak_fence on both sides)
-    constexpr int k = R - 12;
-    if ((uint32_t)k < cnt) base[k] = v[k];
-    if constexpr (k == 10) cnt = 0;
-  }
-  DEVI void flush() {
-#pragma unroll
-    for (int k = 0; k < 11; ++k)
-      if ((uint32_t)k < cnt) base[k] = v[k];
-    cnt = 0;
-  }
-};
+// Diagnostic builds (tools/build_variant.sh + tools/sponge_ab.py; wrong bytes, timing only):
+//   P3G_DIAG_EXPAND_NOSTORE  the fast squeeze folds each block into a register instead of storing
+//   P3G_DIAG_JR_NOLOAD       k_jr issues no LDS-DMA window fills (absorbs whatever LDS holds)
+//   P3G_DIAG_JR_NOABSORB     k_jr absorbs constants instead of reading its LDS window
+#ifndef P3G_DIAG_EXPAND_NOSTORE
+#define P3G_DIAG_EXPAND_NOSTORE 0
+#endif
+#ifndef P3G_DIAG_JR_NOLOAD
+#define P3G_DIAG_JR_NOLOAD 0
+#endif
+#ifndef P3G_DIAG_JR_NOABSORB
+#define P3G_DIAG_JR_NOABSORB 0
+#endif
 
 template <>
 struct SqueezeVec<Field128Ops> {
@@ -134,6 +124,9 @@ struct SqueezeVec<Field128Ops> {
     uint32_t cnt = 0;
     uint32_t parity = 0;
     uint64_t carry = 0;
+#if P3G_DIAG_EXPAND_NOSTORE
+    uint64_t sink = 0;
+#endif
     while (true) {
       bool fast = !exact && cnt + 11u <= n;
       if (parity == 0) {
@@ -146,6 +139,14 @@ struct SqueezeVec<Field128Ops> {
       }
       if (fast) {
         uint64_t* o = reinterpret_cast<uint64_t*>(out + (size_t)cnt * 16);
+#if P3G_DIAG_EXPAND_NOSTORE  // diagnostic build only (tools/sponge_ab.py): fold instead of storing
+        if (true) {
+#pragma unroll
+          for (int k = 0; k < 21; ++k) sink ^= s[k];
+          carry = s[20];
+          cnt += parity == 0 ? 10u : 11u;
+        } else
+#endif
         if (parity == 0) {
 #pragma unroll
           for (int k = 0; k < 10; ++k)
@@ -190,6 +191,9 @@ struct SqueezeVec<Field128Ops> {
       parity ^= 1u;
       next(s);
     }
+#if P3G_DIAG_EXPAND_NOSTORE
+    st64(out, sink);
+#endif
   }
 };
 
@@ -224,77 +228,6 @@ DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out, const Xof& x, bo
   SqueezeVec<FO>::run(s, n, out, exact, KeccakNext{x});
 }
 
-// SqueezeVec<Field128Ops>'s loop with the fast path's stores deferred into the next permutation
-// (PendingStores).  Same output as squeeze_vec: a block whose elements are not all provably
-// canonical takes the exact per-element path, stored at once.
-DEVI void squeeze_vec_f128_deferred(uint64_t s[25], uint32_t n, uint8_t* out, const Xof& x) {
-  using FO = Field128Ops;
-  PendingStores pend;
-  uint32_t cnt = 0, parity = 0;
-  uint64_t carry = 0;
-  while (true) {
-    bool fast = cnt + 11u <= n;
-    if (parity == 0) {
-#pragma unroll
-      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 1]);
-    } else {
-      fast &= hi_ok(s[0]);
-#pragma unroll
-      for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
-    }
-    if (fast) {
-      pend.base = reinterpret_cast<ulonglong2*>(out + (size_t)cnt * 16);
-      if (parity == 0) {
-#pragma unroll
-        for (int k = 0; k < 10; ++k) pend.v[k] = make_ulonglong2(s[2 * k], s[2 * k + 1]);
-        carry = s[20];
-        pend.cnt = 10u;
-        cnt += 10u;
-      } else {
-        pend.v[0] = make_ulonglong2(carry, s[0]);
-#pragma unroll
-        for (int k = 0; k < 10; ++k) pend.v[k + 1] = make_ulonglong2(s[2 * k + 1], s[2 * k + 2]);
-        pend.cnt = 11u;
-        cnt += 11u;
-      }
-    } else if (parity == 0) {
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
-        if (cnt < n && FO::is_canonical(e)) {
-          FO::store(out + (size_t)cnt * 16, e);
-          ++cnt;
-        }
-      }
-      carry = s[20];
-    } else {
-      {
-        F128 e = FO::from_u64x2(carry, s[0]);
-        if (cnt < n && FO::is_canonical(e)) {
-          FO::store(out + (size_t)cnt * 16, e);
-          ++cnt;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
-        if (cnt < n && FO::is_canonical(e)) {
-          FO::store(out + (size_t)cnt * 16, e);
-          ++cnt;
-        }
-      }
-    }
-    if (cnt >= n) break;
-    parity ^= 1u;
-    keccak_x_h(s, x, pend);
-  }
-  pend.flush();
-}
-
-#ifndef P3G_EXPAND_DEFER
-#define P3G_EXPAND_DEFER 0
-#endif
-
 // XOF(seed, dst(usage), binder=[byte]) expanded into n elements (helper share expansion).
 template <class FO>
 DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed_lo,
@@ -307,12 +240,7 @@ DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed
   m.pad(26, x);
   uint64_t s[25];
   sponge_one_block(s, m, x);
-  if constexpr (P3G_EXPAND_DEFER != 0 && FO::ES == 16) {
-    if (!exact) squeeze_vec_f128_deferred(s, n, out, x);
-    else squeeze_vec<FO>(s, n, out, x, exact);
-  } else {
-    squeeze_vec<FO>(s, n, out, x, exact);
-  }
+  squeeze_vec<FO>(s, n, out, x, exact);
 }
 
 // derive_seed(0^16, dst6, part0 || part1)   (prio Prio3::derive_joint_rand_seed)
@@ -459,23 +387,9 @@ DEVI void acc_u64(uint32_t& lo, uint32_t& hi, uint32_t& cy, uint64_t x) {
       : "vcc");
 }
 
-#ifndef P3G_JR_SPREAD
-#define P3G_JR_SPREAD 0
-#endif
-// P3G_JR_SPREAD: k_jr issues the 11 LDS-DMA pieces of the next window one per round (rounds
-// 12..22) inside the permutation instead of as one burst before it.
-template <class SP>
-struct SpreadHook {
-  SP* sp;
-  int64_t b;
-  bool on;
-  template <int R>
-  static constexpr bool active() { return R >= 12 && R < 23; }
-  template <int R>
-  DEVI void after() {
-    if (on) (*sp)(b, R - 12);
-  }
-};
+// Buffer resource word 3 for raw (stride 0) buffer loads on gfx9-family parts (gfx950):
+// DATA_FORMAT = 32, everything else 0.
+constexpr int kBufRsrcWord3 = 0x00020000;
 
 constexpr uint32_t kJrWin = 176;  // bytes per report in the LDS window (22 words)
 constexpr uint32_t kJrWaveLds = 64 * kJrWin;
@@ -488,12 +402,13 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
                                             uint8_t* spec_cy) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t r0w = blockIdx.x * blockDim.x + (tid & ~63u);  // first report of this wave
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave in block (uniform)
+  const uint32_t r0w = blockIdx.x * blockDim.x + 64u * wv;       // first report of this wave
   if (r0w >= n) return;                                          // wave-uniform
   const uint32_t r = r0w + lane;
   const bool live = r < n && (!status || status[r] == ST_OK);
   const uint32_t rr = r < n ? r : n - 1u;
-  uint8_t* win = smem + (tid >> 6) * kJrWaveLds;
+  uint8_t* win = smem + wv * kJrWaveLds;
 
   const uint8_t* data = meas.at(rr);
   const uint32_t nbytes = cfg.meas_len * cfg.es;
@@ -503,15 +418,23 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
   const int64_t padw = total >> 3;
   const uint64_t padv = (uint64_t)cfg.xof.pad << ((total & 7) * 8);
 
-  // LDS-DMA piece q of this lane: flat piece P = 64q + lane = (row, k) with 11 pieces per row.
-  // Recomputed per fill from lane = 11 la + lb (a few VALU ops per piece) instead of holding 11
-  // offsets live across the permutation: k_jr must stay <= 168 VGPRs (3 waves per SIMD).
+  // LDS-DMA piece q of this lane: flat piece P = 64q + lane = (row, k) with 11 pieces per row,
+  // lane = 11 la + lb:  row = la + cq + wrap, k = lb + dq - 11 wrap, wrap = (lb + dq >= 11),
+  // where 64q = 11 cq + dq.  A full wave (64 live rows) reads piece q at the per-lane offset
+  //   la mstride + 16 lb  +  (cq mstride + 16 dq)  +  wrap (mstride - 176)
+  // = one loop-invariant VGPR + a scalar + a select: buffer_load ... lds with the window's source
+  // as the (scalar) buffer base, 2 VALU per piece (the general form, kept for the last partial
+  // wave whose rows clamp at rlim, spends ~14 incl. a quarter-rate v_mul_lo_u32 and two 64-bit
+  // adds).  k_jr must stay <= 168 VGPRs (3 waves per SIMD).
   const uint32_t la0 = lane / 11u, lb0 = lane - 11u * la0;
   const uint32_t rlim = (n - r0w < 64u ? n - r0w : 64u) - 1u;  // last valid row of the wave
+  const bool full_wave = rlim == 63u;                             // wave-uniform
   const uint32_t mstride = (uint32_t)meas.stride;
   const uint8_t* wbase = meas.base + (size_t)r0w * meas.stride;
+  const uint32_t lofs = la0 * mstride + 16u * lb0;
+  const uint32_t wdelta = mstride - 176u;
   auto is_fast = [&](int64_t b) { return (b >= 1) && (21 * b + 15 < nd) && (21 * b + 20 < padw); };
-  // one LDS-DMA piece q (1 KB: 64 lanes x 16 B) of the window of block b
+  // one LDS-DMA piece q (1 KB: 64 lanes x 16 B) of the window of block b, any wave
   auto stage_piece = [&](int64_t b, int q) {
     const uint8_t* src = wbase + 8 * (21 * b - 6);
     // opaque copies: keep LICM from hoisting the 11 per-lane offsets out of the loop
@@ -523,13 +446,35 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
     const uint32_t wrap = t >= 11u ? 1u : 0u;
     const uint32_t row = min(la + cq + wrap, rlim);
     const uint32_t k = t - 11u * wrap;
-    __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(src + (row * mstride + 16u * k)),
-        (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, 0, 0);
+    if (!P3G_DIAG_JR_NOLOAD)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(src + (row * mstride + 16u * k)),
+          (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, 0, 0);
+  };
+  auto stage_full = [&](int64_t b) {  // a full wave: scalar base + 2 VALU per piece
+    const uint8_t* src = wbase + 8 * (21 * b - 6);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 64u * mstride, kBufRsrcWord3);
+    uint32_t lo, lb;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "v"(lofs));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lb) : "v"(lb0));
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      const uint32_t cq = (64u * q) / 11u, dq = (64u * q) % 11u;
+      const uint32_t vo = lo + (lb + dq >= 11u ? wdelta : 0u);
+      if (!P3G_DIAG_JR_NOLOAD)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, vo,
+            cq * mstride + 16u * dq, 0, 0);
+    }
   };
   auto stage = [&](int64_t b) {  // window <- words [21b-6, 21b+16) of every row of the wave
+    if (full_wave) {
+      stage_full(b);
+    } else {
 #pragma unroll
-    for (int q = 0; q < 11; ++q) stage_piece(b, q);
+      for (int q = 0; q < 11; ++q) stage_piece(b, q);
+    }
   };
 
 
@@ -540,12 +485,17 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
     if (is_fast(b)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint64_t* L = reinterpret_cast<const uint64_t*>(win + lane * kJrWin);
+      if (P3G_DIAG_JR_NOABSORB) {
+#pragma unroll
+        for (int w = 0; w < 21; ++w) s[w] ^= (uint64_t)b * 0x9E3779B97F4A7C15ull + w;
+      } else {
       uint64_t prev = L[0];
 #pragma unroll
       for (int w = 0; w < 21; ++w) {
         const uint64_t cur = L[w + 1];
         s[w] ^= (prev >> 48) | (cur << 16);
         prev = cur;
+      }
       }
       if (spec_lo != nullptr) {
         // Speculative accumulation: column sums of the window's 21 new words over the wave's 64
@@ -612,18 +562,11 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
         s[w] ^= v;
       }
     }
-    if constexpr (P3G_JR_SPREAD != 0) {
-      const bool refill = is_fast(b + 1);  // wave-uniform
-      if (refill) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      SpreadHook<decltype(stage_piece)> hook{&stage_piece, b + 1, refill};
-      keccak_x_h(s, cfg.xof, hook);
-    } else {
-      if (is_fast(b + 1)) {  // refill the window (its reads above have completed) under the permutation
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        stage(b + 1);
-      }
-      keccak_x(s, cfg.xof);
+    if (is_fast(b + 1)) {  // refill the window (its reads above have completed) under the permutation
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stage(b + 1);
     }
+    keccak_x(s, cfg.xof);
   }
   if (!live) return;
   const uint64_t plo = s[0], phi = s[1];

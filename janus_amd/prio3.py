@@ -94,6 +94,29 @@ def _ptr(a) -> Optional[int]:
     raise TypeError(f"unsupported buffer type {type(a)}")
 
 
+def _pitched_rows(a, n: int, width: int, what: str):
+    """(buffer, row pitch) of an (n, width) uint8 view whose rows may sit `pitch` >= width bytes
+    apart (a column slice of a wider, e.g. 128-B-aligned, buffer: numpy or torch, host or
+    device); anything else goes through `_as_u8` and is packed (pitch = width)."""
+    shp = getattr(a, "shape", None)
+    if shp is not None and len(shp) == 2 and tuple(shp) == (n, width) and n > 1:
+        if isinstance(a, np.ndarray) and a.dtype == np.uint8 and a.strides[1] == 1:
+            return a, a.strides[0]
+        if hasattr(a, "data_ptr") and getattr(a, "element_size", lambda: 0)() == 1 and \
+                a.stride(1) == 1:
+            return a, a.stride(0)
+    return _as_u8(a, n, width, what), width
+
+
+def _row_ptr(a) -> Optional[int]:
+    """Pointer of row 0 of a `_pitched_rows` buffer (rows need only be contiguous inside)."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return _ptr(a)
+
+
 def _nbytes(a) -> int:
     if isinstance(a, np.ndarray):
         return a.nbytes
@@ -124,6 +147,14 @@ class PrepareState:
               "state_create")
         self._h = h
         self._keep = None  # keeps device inputs referenced until prepare_next
+        self._pitch = 0
+
+    def set_input_pitch(self, pitch: int):
+        """Row pitch of the input shares the next calls read (0 = packed; else a multiple of 16
+        that is >= the share length): prio3gpu_state_set_input_pitch."""
+        if pitch != self._pitch:
+            check(lib().prio3gpu_state_set_input_pitch(self._h, pitch), "state_set_input_pitch")
+            self._pitch = pitch
 
     def close(self):
         if getattr(self, "_h", None):
@@ -295,8 +326,12 @@ class Prio3Gpu:
         """prepare_init's XOF phase (query + joint randomness, helper expansion); `status` (n,)
         uint8, host or device; inputs must stay valid until prepare_init_query."""
         n = _nbytes(status)
+        s = self.sizes
+        in_len = s.leader_input_share if state.agg_id == 0 else s.helper_input_share
+        input_shares, pitch = _pitched_rows(input_shares, n, in_len, "input shares")
+        state.set_input_pitch(0 if pitch == in_len else pitch)
         check(lib().prio3gpu_prepare_init_xof(self._ctx, state._h, n, _ptr(nonces),
-                                              _ptr(public_shares), _ptr(input_shares),
+                                              _ptr(public_shares), _row_ptr(input_shares),
                                               _ptr(status)), "prepare_init_xof")
         state._keep = input_shares
 
@@ -324,7 +359,8 @@ class Prio3Gpu:
         nonces = _as_u8(nonces, n, 16, "nonces")
         public_shares = _as_u8(public_shares, n, s.public_share, "public shares") \
             if s.public_share else None
-        input_shares = _as_u8(input_shares, n, in_len, "input shares")
+        input_shares, pitch = _pitched_rows(input_shares, n, in_len, "input shares")
+        state.set_input_pitch(0 if pitch == in_len else pitch)
         st = np.zeros(n, dtype=np.uint8) if status is None else status
         if out_prep_shares is not None:
             prep = out_prep_shares[:n]
@@ -334,7 +370,7 @@ class Prio3Gpu:
         else:
             prep = np.zeros((n, s.prep_share), dtype=np.uint8) if want_prep_shares else None
         check(lib().prio3gpu_prepare_init(self._ctx, state._h, n, _ptr(nonces),
-                                          _ptr(public_shares), _ptr(input_shares), _ptr(prep),
+                                          _ptr(public_shares), _row_ptr(input_shares), _ptr(prep),
                                           _ptr(st)), "prepare_init")
         state._keep = input_shares
         return prep, st
@@ -376,7 +412,9 @@ class Prio3Gpu:
         n = _nbytes(nonces) // 16
         nonces = _as_u8(nonces, n, 16, "nonces")
         pub = _as_u8(public_shares, n, s.public_share, "public shares") if s.public_share else None
-        hs = _as_u8(helper_input_shares, n, s.helper_input_share, "helper input shares")
+        hs, pitch = _pitched_rows(helper_input_shares, n, s.helper_input_share,
+                                  "helper input shares")
+        state.set_input_pitch(0 if pitch == s.helper_input_share else pitch)
         lp = _as_u8(leader_prep_shares, n, s.prep_share, "leader prep shares")
         st = np.zeros(n, dtype=np.uint8) if status is None else status
         msgs = out_prep_msgs
@@ -387,7 +425,7 @@ class Prio3Gpu:
             slots = batch_slots if not isinstance(batch_slots, np.ndarray) else \
                 np.ascontiguousarray(batch_slots, dtype=np.uint32)
         check(lib().prio3gpu_helper_init(self._ctx, state._h, n, _ptr(nonces), _ptr(pub),
-                                         _ptr(hs), _ptr(lp), _ptr(slots), _ptr(msgs), _ptr(st),
+                                         _row_ptr(hs), _ptr(lp), _ptr(slots), _ptr(msgs), _ptr(st),
                                          agg._h if agg else None), "helper_init")
         return msgs, st
 

@@ -155,6 +155,7 @@ extern "C" {
     pub fn prio3gpu_state_create(ctx: *mut prio3gpu_ctx, agg_id: c_int, capacity: usize,
                                  out: *mut *mut prio3gpu_state) -> c_int;
     pub fn prio3gpu_state_destroy(st: *mut prio3gpu_state) -> c_int;
+    pub fn prio3gpu_state_set_input_pitch(st: *mut prio3gpu_state, pitch: usize) -> c_int;
     pub fn prio3gpu_agg_create(ctx: *mut prio3gpu_ctx, num_slots: u32,
                                out: *mut *mut prio3gpu_agg) -> c_int;
     pub fn prio3gpu_agg_destroy(agg: *mut prio3gpu_agg) -> c_int;

@@ -443,3 +443,45 @@ def test_report_checksum_and_interval():
             assert (start, dur) == (0, 0)
     agg.reset()
     assert agg.read_reports(0) == (bytes(32), (0, 0))
+
+
+@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "sum32", "count", "fp16_3"])
+def test_pitched_input_shares_bit_exact(name):
+    """Input shares at a row pitch > the share length (prio3gpu_state_set_input_pitch): a caller
+    decoding leader shares into 128-B-aligned rows gets the same prep shares, prep messages and
+    aggregates as with packed rows; host and device buffers; the helper's seeds too."""
+    import torch
+    from janus_amd._lib import Prio3GpuError
+    b = batch(name)
+    v = gpu_vdaf(b)
+    s = v.sizes
+    lp_pitch = (s.leader_input_share + 127) // 128 * 128 + 128
+    rows = np.zeros((b.n, lp_pitch), np.uint8)
+    rows[:, :s.leader_input_share] = b.leader_in
+    ls = v.new_state(0, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, rows[:, :s.leader_input_share])
+    assert (lst == 0).all()
+    np.testing.assert_array_equal(lp, b.leader_prep)
+    d_rows = torch.from_numpy(rows).cuda()
+    ls2 = v.new_state(0, b.n)
+    lp2, lst2 = v.prepare_init(ls2, b.nonces, b.public, d_rows[:, :s.leader_input_share])
+    assert (lst2 == 0).all()
+    np.testing.assert_array_equal(lp2, b.leader_prep)
+    hrows = torch.zeros((b.n, 64), dtype=torch.uint8)
+    hrows[:, :s.helper_input_share] = torch.from_numpy(b.helper_in)
+    hs = v.new_state(1, b.n)
+    hagg = v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, b.nonces, b.public, hrows.cuda()[:, :s.helper_input_share], lp,
+                              agg=hagg)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(msgs, b.prep_msg)
+    lagg = v.new_aggregate(1)
+    v.prepare_next(ls2, msgs, lst2, want_output_shares=False, agg=lagg)
+    assert lagg.read(0)[0] == expected_aggregate(b, "leader")[0]
+    assert hagg.read(0)[0] == expected_aggregate(b, "helper")[0]
+    # a packed call on the same state after a pitched one reads packed rows again
+    lp3, _ = v.prepare_init(ls2, b.nonces, b.public, b.leader_in)
+    np.testing.assert_array_equal(lp3, b.leader_prep)
+    for bad in (s.leader_input_share - 16, lp_pitch + 8):
+        with pytest.raises(Prio3GpuError):
+            ls2.set_input_pitch(bad)

@@ -25,6 +25,12 @@ pass() {  # pass NAME "COUNTERS"
   case $rc in 124|137|134|139|-6|-11) exit $rc ;; esac
   return 0
 }
+timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d "$O/raw_trace" -o run -- python3 "$R/bench.py" $ARGS > "$O/trace.log" 2>&1
+trc=$?
+echo "trace rc=$trc"
+case $trc in 124|137|134|139) exit $trc ;; esac
+find "$O/raw_trace" -name "*kernel_trace.csv" -exec cp {} "$O/kernel_trace.csv" \;
+rm -rf "$O/raw_trace"
 pass sqA "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
 pass sqB "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"
 pass sqC "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_ACTIVE_INST_FLAT SQ_INSTS_SMEM SQ_IFETCH"
