@@ -104,13 +104,21 @@ DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 
 // Diagnostic builds (tools/build_variant.sh + tools/sponge_ab.py; wrong bytes, timing only):
 //   P3G_DIAG_EXPAND_NOSTORE  the fast squeeze folds each block into a register instead of storing
+//   P3G_DIAG_EXPAND_TILED    k_expand writes the meas share as element-major 64-report tiles
 //   P3G_DIAG_JR_NOLOAD       k_jr issues no LDS-DMA window fills (absorbs whatever LDS holds)
+//   P3G_DIAG_JR_NOWAIT       k_jr reads its window without waiting for the fill (stale bytes)
 //   P3G_DIAG_JR_NOABSORB     k_jr absorbs constants instead of reading its LDS window
 #ifndef P3G_DIAG_EXPAND_NOSTORE
 #define P3G_DIAG_EXPAND_NOSTORE 0
 #endif
+#ifndef P3G_DIAG_EXPAND_TILED
+#define P3G_DIAG_EXPAND_TILED 0
+#endif
 #ifndef P3G_DIAG_JR_NOLOAD
 #define P3G_DIAG_JR_NOLOAD 0
+#endif
+#ifndef P3G_DIAG_JR_NOWAIT
+#define P3G_DIAG_JR_NOWAIT 0
 #endif
 #ifndef P3G_DIAG_JR_NOABSORB
 #define P3G_DIAG_JR_NOABSORB 0
@@ -118,7 +126,9 @@ DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 
 template <>
 struct SqueezeVec<Field128Ops> {
-  template <class Next>
+  // ESTR: bytes from one output element to the next: 16 (a report's row) or 1024 (element-major
+  // 64-report tiles, where a wave's lanes store one contiguous 1 KB per element).
+  template <class Next, uint32_t ESTR = 16>
   static DEVI void run(uint64_t s[25], uint32_t n, uint8_t* out, bool exact, Next next) {
     using FO = Field128Ops;
     uint32_t cnt = 0;
@@ -138,7 +148,7 @@ struct SqueezeVec<Field128Ops> {
         for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
       }
       if (fast) {
-        uint64_t* o = reinterpret_cast<uint64_t*>(out + (size_t)cnt * 16);
+        uint8_t* o = out + (size_t)cnt * ESTR;
 #if P3G_DIAG_EXPAND_NOSTORE  // diagnostic build only (tools/sponge_ab.py): fold instead of storing
         if (true) {
 #pragma unroll
@@ -150,14 +160,15 @@ struct SqueezeVec<Field128Ops> {
         if (parity == 0) {
 #pragma unroll
           for (int k = 0; k < 10; ++k)
-            *reinterpret_cast<ulonglong2*>(o + 2 * k) = make_ulonglong2(s[2 * k], s[2 * k + 1]);
+            *reinterpret_cast<ulonglong2*>(o + k * ESTR) = make_ulonglong2(s[2 * k], s[2 * k + 1]);
           carry = s[20];
           cnt += 10u;
         } else {
           *reinterpret_cast<ulonglong2*>(o) = make_ulonglong2(carry, s[0]);
 #pragma unroll
           for (int k = 0; k < 10; ++k)
-            *reinterpret_cast<ulonglong2*>(o + 2 * k + 2) = make_ulonglong2(s[2 * k + 1], s[2 * k + 2]);
+            *reinterpret_cast<ulonglong2*>(o + (k + 1) * ESTR) =
+                make_ulonglong2(s[2 * k + 1], s[2 * k + 2]);
           cnt += 11u;
         }
       } else if (parity == 0) {
@@ -165,7 +176,7 @@ struct SqueezeVec<Field128Ops> {
         for (int k = 0; k < 10; ++k) {
           F128 e = FO::from_u64x2(s[2 * k], s[2 * k + 1]);
           if (cnt < n && FO::is_canonical(e)) {
-            FO::store(out + (size_t)cnt * 16, e);
+            FO::store(out + (size_t)cnt * ESTR, e);
             ++cnt;
           }
         }
@@ -174,7 +185,7 @@ struct SqueezeVec<Field128Ops> {
         {
           F128 e = FO::from_u64x2(carry, s[0]);
           if (cnt < n && FO::is_canonical(e)) {
-            FO::store(out + (size_t)cnt * 16, e);
+            FO::store(out + (size_t)cnt * ESTR, e);
             ++cnt;
           }
         }
@@ -182,7 +193,7 @@ struct SqueezeVec<Field128Ops> {
         for (int k = 0; k < 10; ++k) {
           F128 e = FO::from_u64x2(s[2 * k + 1], s[2 * k + 2]);
           if (cnt < n && FO::is_canonical(e)) {
-            FO::store(out + (size_t)cnt * 16, e);
+            FO::store(out + (size_t)cnt * ESTR, e);
             ++cnt;
           }
         }
@@ -223,13 +234,16 @@ struct KeccakNext {
   DEVI void operator()(uint64_t s[25]) const { keccak_x(s, x); }
 };
 
-template <class FO>
+template <class FO, uint32_t ESTR = FO::ES>
 DEVI void squeeze_vec(uint64_t s[25], uint32_t n, uint8_t* out, const Xof& x, bool exact = false) {
-  SqueezeVec<FO>::run(s, n, out, exact, KeccakNext{x});
+  if constexpr (ESTR == FO::ES)
+    SqueezeVec<FO>::run(s, n, out, exact, KeccakNext{x});
+  else
+    SqueezeVec<FO>::template run<KeccakNext, ESTR>(s, n, out, exact, KeccakNext{x});
 }
 
 // XOF(seed, dst(usage), binder=[byte]) expanded into n elements (helper share expansion).
-template <class FO>
+template <class FO, uint32_t ESTR = FO::ES>
 DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed_lo,
                                  uint64_t seed_hi, uint32_t binder_byte, uint32_t n,
                                  uint8_t* out, const Xof& x, bool exact) {
@@ -240,7 +254,7 @@ DEVI void xof_expand_byte_binder(uint32_t algo_id, uint32_t usage, uint64_t seed
   m.pad(26, x);
   uint64_t s[25];
   sponge_one_block(s, m, x);
-  squeeze_vec<FO>(s, n, out, x, exact);
+  squeeze_vec<FO, ESTR>(s, n, out, x, exact);
 }
 
 // derive_seed(0^16, dst6, part0 || part1)   (prio Prio3::derive_joint_rand_seed)
@@ -365,6 +379,14 @@ __global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t ag
   const uint8_t* hs = helper_shares.at(r);
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), agg_id,
                              cfg.proof_len, out_proof.at(r), cfg.xof, cfg.exact_squeeze);
+#if P3G_DIAG_EXPAND_TILED  // diagnostic: element-major 64-report tiles (consumers not adapted)
+  if constexpr (FO::ES == 16) {
+    uint8_t* t = out_meas.base + (size_t)(r >> 6) * 64u * out_meas.stride + (r & 63u) * 16u;
+    xof_expand_byte_binder<FO, 1024>(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8),
+                                     agg_id, cfg.meas_len, t, cfg.xof, cfg.exact_squeeze);
+    return;
+  }
+#endif
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8), agg_id,
                              cfg.meas_len, out_meas.at(r), cfg.xof, cfg.exact_squeeze);
 }
@@ -483,7 +505,7 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
   for (int i = 0; i < 25; ++i) s[i] = 0ull;
   for (int64_t b = 0; b < nblocks; ++b) {
     if (is_fast(b)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!P3G_DIAG_JR_NOWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint64_t* L = reinterpret_cast<const uint64_t*>(win + lane * kJrWin);
       if (P3G_DIAG_JR_NOABSORB) {
 #pragma unroll
@@ -1748,6 +1770,9 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
       Wide wa, wb;
       wide_zero(wa);
       wide_zero(wb);
+      // each element is loaded just before its MACs: the pass hides HBM latency with occupancy
+      // (78 VGPRs); loading one or three calls ahead (84-88 VGPRs) ran 5-8 % slower
+      // (profiles/r03/ab_wires_ahead*.log)
       uint32_t k = h;
       for (; k + H < C; k += 2 * H) {  // calls k and k+H; only the last call can be padded
         const uint32_t i0 = k * c + j, i1 = (k + H) * c + j;

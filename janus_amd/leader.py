@@ -86,6 +86,8 @@ class LeaderStepped:
     d_in: object = None              # device copy of the leader input shares (kept alive)
     slots: Optional[np.ndarray] = None
     times_ms: dict = field(default_factory=dict)
+    prep: object = None              # prep shares between prepare and encode (pinned buffer view)
+    pbuf: object = None
 
 
 class LeaderAggregateInit:
@@ -152,6 +154,11 @@ class LeaderAggregateInit:
             self._states = []
             self._prep_bufs = []
 
+    def _return_prep_buf(self, b):
+        if b is not None:
+            with self._lock:
+                self._prep_bufs.append(b)
+
     def _prep_buf(self, n: int) -> np.ndarray:
         """A pinned (>= n, prep_share) buffer for prepare_init's output (the device -> host copy
         of 2,896 B per SumVec report is then DMA); buffers are reused once the request that
@@ -169,6 +176,17 @@ class LeaderAggregateInit:
     # -- steps ---------------------------------------------------------------------------------------
     def init(self, job: LeaderJob, d_in=None) -> LeaderStepped:
         """Steps 1-3: pre-checks, GPU prepare_init, request bytes."""
+        st = self.prepare(job, d_in)
+        try:
+            self.encode(st)
+        except BaseException:
+            self._release(st.state)
+            raise
+        return st
+
+    def prepare(self, job: LeaderJob, d_in=None) -> LeaderStepped:
+        """Steps 1-2: pre-checks and GPU prepare_init; the prep shares wait in a pinned buffer
+        for `encode` (which may run on another thread while the GPU takes the next job)."""
         import time
         n = job.n
         if n == 0:
@@ -189,23 +207,36 @@ class LeaderAggregateInit:
             prep, status = self.vdaf.prepare_init(state, job.nonces,
                                                   job.public if s.public_share else None, d_in,
                                                   status=status, out_prep_shares=pbuf)
-            t2 = time.perf_counter()
-            req = C.encode_agg_init_req_packed(self.query_type, self.batch_id, b"", job.nonces,
-                                               job.times, job.public, job.hpke_config_ids,
-                                               job.encs, job.enc_offsets, job.payloads,
-                                               job.payload_offsets, prep, status)
         except BaseException:
             self._release(state)
+            self._return_prep_buf(pbuf)
             raise
-        finally:
-            self._prep_bufs.append(pbuf)  # the prep shares live on in the request bytes
-        t3 = time.perf_counter()
+        t2 = time.perf_counter()
         slots = None
         if self.batch_slot_of is not None:
             slots = np.ascontiguousarray(self.batch_slot_of(np.asarray(job.times)), np.uint32)
-        return LeaderStepped(job, state, status, req, d_in, slots,
-                             {"stage": (t1 - t0) * 1e3, "prepare_init": (t2 - t1) * 1e3,
-                              "encode": (t3 - t2) * 1e3})
+        st = LeaderStepped(job, state, status, b"", d_in, slots,
+                           {"stage": (t1 - t0) * 1e3, "prepare_init": (t2 - t1) * 1e3})
+        st.prep = prep
+        st.pbuf = pbuf
+        return st
+
+    def encode(self, st: LeaderStepped) -> bytes:
+        """Step 3: the AggregationJobInitializeReq of a prepared job (its prep-share buffer is
+        returned to the pool: the shares live on in the request bytes)."""
+        import time
+        t0 = time.perf_counter()
+        job = st.job
+        try:
+            st.request = C.encode_agg_init_req_packed(
+                self.query_type, self.batch_id, b"", job.nonces, job.times, job.public,
+                job.hpke_config_ids, job.encs, job.enc_offsets, job.payloads, job.payload_offsets,
+                st.prep, st.status)
+        finally:
+            self._return_prep_buf(st.pbuf)
+            st.prep = st.pbuf = None
+        st.times_ms["encode"] = (time.perf_counter() - t0) * 1e3
+        return st.request
 
     def finish(self, st: LeaderStepped, resp: bytes, agg: AggregateShares) -> np.ndarray:
         """Steps 5-6.  Raises Prio3GpuError when the response does not answer exactly the sent
@@ -232,9 +263,13 @@ class LeaderAggregateInit:
         return self.finish(st, send(st.request), agg)
 
     def run_jobs(self, jobs: Sequence[LeaderJob], send: Callable[[bytes], bytes],
-                 agg: AggregateShares, stats: Optional[list] = None) -> List[object]:
-        """Pipelined over jobs: H2D of job k+1 || GPU prepare_init of job k; helper round trip
-        of job k || GPU work of job k+1.  `stats`, if given, receives each job's stage times.
+                 agg: AggregateShares, stats: Optional[list] = None,
+                 stage_ahead: int = 2) -> List[object]:
+        """Pipelined over jobs: the H2D copies of the next `stage_ahead` jobs queue on the copy
+        stream behind the current one (the copy engine never waits for the driver thread), GPU
+        prepare_init of job k runs while job k-1's request is encoded and sent on the network
+        worker, and job k-1's response is finished after job k is queued.  `stats`, if given,
+        receives each job's stage times.
 
         Entry k is job k's per-report final statuses, or the exception that failed job k alone:
         an empty job (EmptyAggregation), a response that does not answer the sent reports
@@ -245,16 +280,21 @@ class LeaderAggregateInit:
         out: List[object] = [None] * len(jobs)
         if not jobs:
             return out
+        ahead = max(1, stage_ahead)
         with ThreadPoolExecutor(max_workers=1) as h2d, ThreadPoolExecutor(max_workers=1) as net:
-            staged = h2d.submit(self.stage, jobs[0])
+            staged = [h2d.submit(self.stage, jobs[i]) for i in range(min(ahead, len(jobs)))]
             inflight = None  # (job index, LeaderStepped, response future)
+
+            def encode_send(st):
+                return send(self.encode(st))
 
             def finish_inflight():
                 k0, st0, fut0 = inflight
                 try:
                     resp = fut0.result()
-                except Exception as e:  # the helper round trip failed: this job alone
+                except Exception as e:  # encoding or the helper round trip failed: this job alone
                     self._release(st0.state)
+                    self._return_prep_buf(st0.pbuf)
                     st0.d_in = None
                     out[k0] = e
                     return
@@ -268,18 +308,18 @@ class LeaderAggregateInit:
             try:
                 for k in range(len(jobs)):
                     try:
-                        d_in = staged.result()
+                        d_in = staged.pop(0).result()
                     except Exception as e:
                         d_in = e
-                    if k + 1 < len(jobs):
-                        staged = h2d.submit(self.stage, jobs[k + 1])
+                    if k + ahead < len(jobs):
+                        staged.append(h2d.submit(self.stage, jobs[k + ahead]))
                     started = None
                     if isinstance(d_in, Exception):
                         out[k] = d_in
                     else:
                         try:
-                            st = self.init(jobs[k], d_in)
-                            started = (k, st, net.submit(send, st.request))
+                            st = self.prepare(jobs[k], d_in)
+                            started = (k, st, net.submit(encode_send, st))
                         except Prio3GpuError as e:  # EmptyAggregation, a rejected batch
                             out[k] = e
                     if inflight is not None:

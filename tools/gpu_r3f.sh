@@ -18,3 +18,7 @@ for l in open('gpurun_out/bench_r3f.log'):
     if l.startswith('{'):
         d=json.loads(l); print('bench', d['value'], 'ms/step', d['ms_per_step']); print(' ', d['kernels_ms_per_step'])
 "
+for v in tile nost; do
+  PRIO3GPU_LIB=janus_amd/lib/libprio3gpu_$v.so timeout -k 10 240 python -u tools/sponge_ab.py --label $v >> gpurun_out/sponge_r3f.log 2> gpurun_out/sponge_r3f.err || { tail -5 gpurun_out/sponge_r3f.err; exit 1; }
+  tail -1 gpurun_out/sponge_r3f.log
+done
