@@ -17,6 +17,7 @@
 #include "errors.h"
 #include "prio3_kernels.h"
 #include "fpvec_kernels.h"
+#include "helper_sponge.h"
 
 using namespace p3g;
 
@@ -142,7 +143,7 @@ enum KernelId {
   KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
   KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
   KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM, KID_JR_RING, KID_FLP_QUERY_LANE,
-  KID_FLP_WIRES_COLS, KID_COUNT
+  KID_FLP_WIRES_COLS, KID_HELPER_SPONGE, KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_helper_xof", "k_jr", "k_flp_weights", "k_flp_query",
@@ -150,7 +151,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
     "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
     "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave", "k_shard_norm",
-    "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols"};
+    "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols", "k_helper_sponge"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -191,6 +192,12 @@ struct prio3gpu_ctx {
   bool fused_helper_all = false;  // A/B: every Field128 type's helper via k_helper_xof (=2)
   uint32_t hx_depth = 2;          // A/B: ring depth of that variant (PRIO3GPU_HX_DEPTH=4)
   bool hx_spec = true;            // A/B: k_helper_xof's storer column sums (PRIO3GPU_HX_SPEC=0: off)
+  // Sum/SumVec/Histogram helper: expansion + joint-rand-part sponges in one pass (k_helper_sponge,
+  // PRIO3GPU_HELPER_SPONGE=1).  Off: measured no faster than k_expand + k_jr (SumVec 72.7 vs
+  // 71.7 ms, Histogram 8.2 vs 7.8, Sum 2.88 vs 2.85 ms/step; 188 VGPRs = 2 waves/SIMD,
+  // profiles/r03/sponge_helper_fused_r3i.log, bench_r3j_*.log)
+  bool helper_sponge = false;
+  bool force_fallback = false;    // test switch (PRIO3GPU_TEST_FALLBACK=1): every lane falls back
   size_t hx_lds = 0;         // tuning: dynamic LDS per k_helper_xof block (PRIO3GPU_HX_LDS)
   // Latency-bound sponge launches with fewer waves than CUs (FixedPoint: a few thousand reports)
   // take one CU per workgroup: the dispatcher otherwise packs several workgroups, and the two
@@ -620,6 +627,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     st->spec_e1 = se1;
   }
   CRows meas, proof, blinds;
+  const uint32_t* jr_gate = nullptr;
   const size_t in_pitch = input_pitch(st);
   if (st->agg_id == 0) {
     meas = CRows{d_in, in_pitch};
@@ -663,14 +671,30 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
       st->xof_done = true;
       return 0;
     }
+    const uint32_t* gate = nullptr;  // k_expand / k_jr run only if the fused pass fell back
+    if constexpr (FO::ES == 16) {
+      if (c->helper_sponge && g.jr_len > 0 && g.kind != KIND_FPVEC) {
+        CHK(c->fallback.ensure(4));
+        uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
+        HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
+        PROF(KID_HELPER_SPONGE);
+        hipLaunchKernelGGL(k_helper_sponge, grid1(n, TPB), dim3(TPB), (TPB / 64) * kJrWaveLds,
+                           c->stream, g, N, CRows{d_in, in_pitch}, nonces, pub, mo, po,
+                           Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
+                           Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb, spec_lo, spec_cy,
+                           2u * se0, 2u * se1, c->force_fallback ? 1u : 0u);
+        gate = fb;
+      }
+    }
     {
       PROF(KID_EXPAND);
       hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
-                         (uint32_t)st->agg_id, CRows{d_in, in_pitch}, mo, po, d_status);
+                         (uint32_t)st->agg_id, CRows{d_in, in_pitch}, mo, po, d_status, gate);
     }
     meas = CRows{mo.base, mo.stride};
     proof = CRows{po.base, po.stride};
     blinds = CRows{d_in + 32, in_pitch};
+    jr_gate = gate;
   }
   bool ring_done = false;
   if constexpr (FO::ES == 16) {
@@ -697,7 +721,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
       hipLaunchKernelGGL(k_jr<FO>, grid1(n, tpb), dim3(tpb), jr_lds, c->stream, g, N,
                          (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
                          Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status,
-                         spec_lo, spec_cy);
+                         spec_lo, spec_cy, jr_gate);
     }
   }
   HIPCHK(hipGetLastError());
@@ -1127,6 +1151,8 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   if (const char* jg = getenv("PRIO3GPU_JR_RING")) c->jr_ring = jg[0] != '0';
   if (const char* hs = getenv("PRIO3GPU_HX_SPEC")) c->hx_spec = hs[0] != '0';
   if (const char* hd = getenv("PRIO3GPU_HX_DEPTH")) c->hx_depth = hd[0] == '4' ? 4u : 2u;
+  if (const char* hp = getenv("PRIO3GPU_HELPER_SPONGE")) c->helper_sponge = hp[0] == '1';
+  if (const char* tf = getenv("PRIO3GPU_TEST_FALLBACK")) c->force_fallback = tf[0] == '1';
   {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
@@ -1137,7 +1163,10 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   // bulk stores are skipped), and the FixedPoint helper runs its exact two-pass XOF.
   const char* ex = getenv("PRIO3GPU_EXACT_SQUEEZE");
   const bool exact_squeeze = ex && ex[0] == '1';
-  if (exact_squeeze) c->fused_helper = false;
+  if (exact_squeeze) {
+    c->fused_helper = false;
+    c->helper_sponge = false;
+  }
   c->device = device;
   memcpy(c->vk, verify_key, 16);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -1761,7 +1790,8 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
   {
     PROF(KID_EXPAND);
     hipLaunchKernelGGL(k_expand<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, 1u,
-                       CRows{d_helper, g.helper_share_len}, hm, hp, (const uint8_t*)nullptr);
+                       CRows{d_helper, g.helper_share_len}, hm, hp, (const uint8_t*)nullptr,
+                       (const uint32_t*)nullptr);
   }
   uint64_t* d_norms = nullptr;  // FixedPointBoundedL2VecSum: squared norm per measurement
   if (g.kind == KIND_FPVEC) {

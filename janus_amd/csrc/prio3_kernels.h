@@ -370,9 +370,13 @@ __global__ void __launch_bounds__(256) k_query_rand(Cfg cfg, uint32_t n, uint64_
 // Helper share expansion: meas share XOF(k_meas, dst1, [agg_id]) and proof share
 // XOF(k_proof, dst2, [agg_id]) (prio prepare_init, Share::Helper arms).
 template <class FO>
+// `gate` (optional): run only if *gate != 0 -- the exact path behind k_helper_sponge, which sets
+// it when a lane met a non-canonical element.
 __global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t agg_id,
                                                 CRows helper_shares, Rows out_meas,
-                                                Rows out_proof, const uint8_t* status) {
+                                                Rows out_proof, const uint8_t* status,
+                                                const uint32_t* gate) {
+  if (gate && *gate == 0u) return;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   if (status && status[r] != ST_OK) return;
@@ -421,8 +425,9 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
                                             CRows public_shares, CRows blinds, CRows meas,
                                             Rows out_part, Rows out_seed, Rows out_jr,
                                             const uint8_t* status, uint64_t* spec_lo,
-                                            uint8_t* spec_cy) {
+                                            uint8_t* spec_cy, const uint32_t* gate) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  if (gate && *gate == 0u) return;  // k_helper_sponge did the work (see k_expand)
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave in block (uniform)
   const uint32_t r0w = blockIdx.x * blockDim.x + 64u * wv;       // first report of this wave

@@ -50,6 +50,21 @@ __global__ void __launch_bounds__(256) k_alignbit(uint32_t* out, uint32_t seed) 
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+__global__ void __launch_bounds__(256) k_perm(uint32_t* out, uint32_t seed) {
+  uint32_t v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = seed * (threadIdx.x + 1) + i;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      v[i] = __builtin_amdgcn_perm(v[i], v[(i + 3) & 15], 0x04030201u + 0x01010101u * (i & 3));
+  }
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r ^= v[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
 __global__ void __launch_bounds__(256) k_mad64(uint32_t* out, uint32_t seed) {
   uint64_t v[8];
   uint32_t m[8];
@@ -123,6 +138,7 @@ int main() {
   CK(hipMalloc(&d, (size_t)blocks * 256 * 4));
   run("int32 bitop3 (xor3)", k_bitop3, 16.0 * ITERS, "lane-ops/s", blocks, d);
   run("int32 alignbit", k_alignbit, 16.0 * ITERS, "lane-ops/s", blocks, d);
+  run("int32 v_perm_b32", k_perm, 16.0 * ITERS, "lane-ops/s", blocks, d);
   run("v_mad_u64_u32", k_mad64, 8.0 * ITERS, "lane-ops/s", blocks, d);
   run("Field128 mont mul", k_f128mul, 4.0 * (ITERS / 16), "mul/s", blocks, d);
   run("Keccak-f[1600]", k_keccak, (double)(ITERS / 64), "perm/s", blocks, d);
