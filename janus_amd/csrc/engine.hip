@@ -1946,7 +1946,7 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
   RCCLCHK(ncclAllReduce(local->counts.p, cm->cgather.p, local->slots, ncclUint64, ncclSum, cm->comm,
                         c->stream));
   // report-ID checksums (XOR) and client-timestamp intervals (min/max): RCCL has neither
-  // reduction, so all-gather the slot meta and fold it on the host below
+  // reduction, so all-gather the slot meta and fold it in k_merge_ranks below
   const size_t mbytes = (size_t)local->slots * sizeof(SlotMeta);
   CHK(cm->mgather.ensure(mbytes * cm->nranks));
   RCCLCHK(ncclAllGather(local->meta.p, cm->mgather.p, mbytes, ncclUint8, cm->comm, c->stream));

@@ -223,8 +223,12 @@ DEVI F128 sqn128(F128 x, int n) {
   for (int i = 0; i < n; ++i) x = Field128Ops::mul(x, x);
   return x;
 }
+#ifndef P3G_DIAG_NOINV
+#define P3G_DIAG_NOINV 0  // diagnostic build (timing only, wrong bytes): the inverse is x itself
+#endif
 DEVI F128 inv_mont128(const F128& x) {
   using FO = Field128Ops;
+  if (P3G_DIAG_NOINV) return x;
   const F128 x2 = FO::mul(FO::mul(x, x), x);    // x^(2^2 - 1)
   const F128 x3 = FO::mul(FO::mul(x2, x2), x);  // 2^3 - 1
   const F128 x6 = FO::mul(sqn128(x3, 3), x3);

@@ -18,17 +18,22 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--reports", type=int, default=393216)
+    ap.add_argument("--reports", type=int, default=0, help="default: 393216 SumVec, else 2^20")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pitch", type=int, default=0)
     ap.add_argument("--label", default=os.path.basename(os.environ.get("PRIO3GPU_LIB", "base")))
+    ap.add_argument("--config", default="sumvec", choices=["sumvec", "histogram", "sum"])
+    ap.add_argument("--query", type=int, default=0,
+                    help="also time the FLP query phase (prepare_init_query) of both aggregators")
     a = ap.parse_args()
     import torch
     from janus_amd._lib import check, lib
-    from janus_amd.prio3 import SUMVEC, Prio3Gpu
-    v = Prio3Gpu(SUMVEC, bytes(range(16)), bits=8, length=1000, chunk_length=89, device=0)
+    from janus_amd.prio3 import HISTOGRAM, SUM, SUMVEC, Prio3Gpu
+    kind, bits, length, chunk = {"sumvec": (SUMVEC, 8, 1000, 89), "histogram": (HISTOGRAM, 0, 256, 16),
+                                 "sum": (SUM, 32, 0, 0)}[a.config]
+    v = Prio3Gpu(kind, bytes(range(16)), bits=bits, length=length, chunk_length=chunk, device=0)
     s = v.sizes
-    B = a.reports
+    B = a.reports or (393216 if a.config == "sumvec" else 1 << 20)
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(1)
@@ -47,16 +52,17 @@ def main():
     cx = v._ctx
     check(L.prio3gpu_prof_enable(cx, 1), "prof")
 
+    prep = torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
+
     def run(leader):
         lst.zero_()
         hst.zero_()
         torch.cuda.synchronize()
-        if leader:
-            check(L.prio3gpu_prepare_init_xof(cx, ls._h, B, P(nonces), P(pub), P(lin), P(lst)),
-                  "leader xof")
-        else:
-            check(L.prio3gpu_prepare_init_xof(cx, hs._h, B, P(nonces), P(pub), P(hin), P(hst)),
-                  "helper xof")
+        st, stt, inp = (ls, lst, lin) if leader else (hs, hst, hin)
+        check(L.prio3gpu_prepare_init_xof(cx, st._h, B, P(nonces), P(pub), P(inp), P(stt)), "xof")
+        if a.query:
+            stt.zero_()  # random shares: keep every report in the query
+            check(L.prio3gpu_prepare_init_query(cx, st._h, B, P(prep), P(stt)), "query")
         check(L.prio3gpu_ctx_sync(cx), "sync")
 
     def read():
@@ -72,12 +78,12 @@ def main():
         for leader in (True, False):
             run(leader)
             for k, (t, n) in read().items():
-                out.setdefault(k + ("_leader" if leader and k == "k_jr" else ""), []).append(t / n)
+                out.setdefault(k + ("_leader" if leader else ""), []).append(t / n)
     res = {k: round(min(x), 3) for k, x in out.items()}
-    perms = {"k_jr": 765, "k_jr_leader": 765, "k_expand": 804}
+    perms = {"k_jr": 765, "k_jr_leader": 765, "k_expand": 804} if a.config == "sumvec" else {}
     rate = {k: round(perms[k] * B / (res[k] * 1e-3) / 1e9, 3) for k in perms if k in res}
-    print(json.dumps({"label": a.label, "reports": B, "pitch": pitch, "ms_per_launch_min": res,
-                      "G_perms_per_s": rate}))
+    print(json.dumps({"label": a.label, "config": a.config, "reports": B, "pitch": pitch,
+                      "ms_per_launch_min": res, "G_perms_per_s": rate}))
 
 
 if __name__ == "__main__":
