@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "inv128.h"
+
 #define DEVI __device__ __forceinline__
 
 struct F128 {
@@ -216,9 +218,14 @@ struct Field64Ops {
   static DEVI F64 from_u32(uint32_t x) { return F64{{x, 0u}}; }
 };
 
-// Field128 inverse x^(p-2), Montgomery form in and out (0 -> 0).  Addition chain over
-// p - 2 = [0xFFFFFFFFFFFFFFE3 | 0xFFFFFFFFFFFFFFFF] = 56 ones, 111000 11, 64 ones:
-// 143 squarings + 12 multiplications.
+// Field128 inverse, Montgomery form in and out (0 -> 0): the canonical inverse y = (xR)^-1 by
+// batched divsteps (inv128.h, ~6K simple ops), then one Montgomery product with R^3 mod p:
+// y R^3 R^-1 = x^-1 R.  P3G_INV_EXP=1 selects the exponentiation x^(p-2) (an addition chain over
+// p - 2 = [0xFFFFFFFFFFFFFFE3 | 0xFFFFFFFFFFFFFFFF] = 56 ones, 111000 11, 64 ones: 143 squarings
+// + 12 multiplications), the form prio computes (same value).
+#ifndef P3G_INV_EXP
+#define P3G_INV_EXP 0
+#endif
 DEVI F128 sqn128(F128 x, int n) {
   for (int i = 0; i < n; ++i) x = Field128Ops::mul(x, x);
   return x;
@@ -229,6 +236,11 @@ DEVI F128 sqn128(F128 x, int n) {
 DEVI F128 inv_mont128(const F128& x) {
   using FO = Field128Ops;
   if (P3G_DIAG_NOINV) return x;
+  if (!P3G_INV_EXP) {
+    F128 y;
+    inv128::inverse(x.w, y.w);
+    return FO::mul(y, F128{{0xFFF6A82Fu, 0xFFFFFFFFu, 0x01054553u, 0u}});  // R^3 mod p
+  }
   const F128 x2 = FO::mul(FO::mul(x, x), x);    // x^(2^2 - 1)
   const F128 x3 = FO::mul(FO::mul(x2, x2), x);  // 2^3 - 1
   const F128 x6 = FO::mul(sqn128(x3, 3), x3);
