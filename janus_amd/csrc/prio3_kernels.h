@@ -1777,13 +1777,16 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
       wide_zero(wb);
       // each element is loaded just before its MACs: the pass hides HBM latency with occupancy
       // (78 VGPRs); loading one or three calls ahead (84-88 VGPRs) ran 5-8 % slower
-      // (profiles/r03/ab_wires_ahead*.log)
+      // (profiles/r03/ab_wires_ahead*.log).  The canonical check is a one-compare pre-filter (an
+      // element >= p has its top word 2^32 - 1), the exact comparison only for a thread that saw
+      // such a word.
+      uint64_t maybe = 0ull;  // lane mask (SGPRs)
       uint32_t k = h;
       for (; k + H < C; k += 2 * H) {  // calls k and k+H; only the last call can be padded
         const uint32_t i0 = k * c + j, i1 = (k + H) * c + j;
         const T x0 = FO::load(xr + (size_t)i0 * ES);
         const T x1 = i1 < cfg.meas_len ? FO::load(xr + (size_t)i1 * ES) : FO::zero();
-        bad |= !FO::is_canonical(x0) || !FO::is_canonical(x1);
+        maybe |= __ballot(x0.w[3] == 0xFFFFFFFFu || x1.w[3] == 0xFFFFFFFFu);
         wide_mac(wa, MM[k], x0);
         wide_mac(wb, LM[k], x0);
         wide_mac(wa, MM[k + H], x1);
@@ -1794,10 +1797,16 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
         const uint32_t i0 = k * c + j;
         if (i0 < cfg.meas_len) {
           const T x0 = FO::load(xr + (size_t)i0 * ES);
-          bad |= !FO::is_canonical(x0);
+          maybe |= __ballot(x0.w[3] == 0xFFFFFFFFu);
           wide_mac(wa, MM[k], x0);
           wide_mac(wb, LM[k], x0);
           if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x0);
+        }
+      }
+      if (maybe) {  // rare: the exact check over this wave's elements
+        for (uint32_t kk = h; kk < C; kk += H) {
+          const uint32_t ii = kk * c + j;
+          if (ii < cfg.meas_len) bad |= !FO::is_canonical(FO::load(xr + (size_t)ii * ES));
         }
       }
       accA = wide_reduce(wa);
