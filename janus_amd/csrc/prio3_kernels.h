@@ -104,12 +104,16 @@ DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 
 // Diagnostic builds (tools/build_variant.sh + tools/sponge_ab.py; wrong bytes, timing only):
 //   P3G_DIAG_EXPAND_NOSTORE  the fast squeeze folds each block into a register instead of storing
+//   P3G_DIAG_EXPAND_FIXED    the fast squeeze stores every block over the row's first 176 bytes
 //   P3G_DIAG_EXPAND_TILED    k_expand writes the meas share as element-major 64-report tiles
 //   P3G_DIAG_JR_NOLOAD       k_jr issues no LDS-DMA window fills (absorbs whatever LDS holds)
 //   P3G_DIAG_JR_NOWAIT       k_jr reads its window without waiting for the fill (stale bytes)
 //   P3G_DIAG_JR_NOABSORB     k_jr absorbs constants instead of reading its LDS window
 #ifndef P3G_DIAG_EXPAND_NOSTORE
 #define P3G_DIAG_EXPAND_NOSTORE 0
+#endif
+#ifndef P3G_DIAG_EXPAND_FIXED
+#define P3G_DIAG_EXPAND_FIXED 0
 #endif
 #ifndef P3G_DIAG_EXPAND_TILED
 #define P3G_DIAG_EXPAND_TILED 0
@@ -148,7 +152,11 @@ struct SqueezeVec<Field128Ops> {
         for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
       }
       if (fast) {
+#if P3G_DIAG_EXPAND_FIXED  // diagnostic: every block's stores hit the row's first 176 bytes
+        uint8_t* o = out + (size_t)(parity * 16u);
+#else
         uint8_t* o = out + (size_t)cnt * ESTR;
+#endif
 #if P3G_DIAG_EXPAND_NOSTORE  // diagnostic build only (tools/sponge_ab.py): fold instead of storing
         if (true) {
 #pragma unroll
