@@ -716,7 +716,9 @@ def main():
     nlaunch = bounds[1] - bounds[0]
     # the PMC passes profile the SHAKE128 build of the command; a TurboSHAKE128 permutation is the
     # last 12 of Keccak-f's 24 rounds: half the ops, twice the measured ceiling rate
-    pmc = load_pmc(args.config) if not turbo else {}
+    # (tools/profile_round.sh profiles the default command: its per-launch bytes only describe
+    # launches of the default batch size)
+    pmc = load_pmc(args.config) if not turbo and B == defaults[args.config][0] else {}
     rf = 0.5 if turbo else 1.0
     if dname in perms and perms[dname]:
         ops = perms[dname] * nlaunch * OPS_PER_PERM * rf
