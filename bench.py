@@ -803,6 +803,10 @@ def main():
         cpu = {"value": round(done / cpu_s, 2), "unit": "reports/s", "cores": nthr,
                "kind": "port",
                "one_thread": round(done1 / cpu1_s, 2),
+               # a whole 8-GPU host (e.g. 256 CPUs) gives each GPU more CPUs than this box's
+               # cgroup share: the speedup at a host's per-GPU CPU count, scaled linearly from
+               # the measured rate, is `value` x cpus_per_gpu_on_host / cores
+               "cpus_per_gpu_on_host_8gpu": (os.cpu_count() or 0) // 8,
                "cpu_model": cpu_model(),
                "host_cpus": host_cpu_info(),
                "sample": f"{done} report preparations ({G} distinct reports, repeated) leader+helper "
@@ -877,6 +881,9 @@ def main():
     }
     if cpu:
         out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        fair = cpu.get("cpus_per_gpu_on_host_8gpu") or 0
+        if fair > cpu["cores"]:  # the same speedup against a linearly scaled fair CPU share
+            out["speedup_vs_cpu_at_host_share"] = round(value / (cpu["value"] * fair / cpu["cores"]), 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:
