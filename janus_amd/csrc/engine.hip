@@ -18,6 +18,7 @@
 #include "prio3_kernels.h"
 #include "fpvec_kernels.h"
 #include "helper_sponge.h"
+#include "wires_mfma.h"
 
 using namespace p3g;
 
@@ -143,7 +144,7 @@ enum KernelId {
   KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
   KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
   KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM, KID_JR_RING, KID_FLP_QUERY_LANE,
-  KID_FLP_WIRES_COLS, KID_HELPER_SPONGE, KID_COUNT
+  KID_FLP_WIRES_COLS, KID_HELPER_SPONGE, KID_FLP_WIRES_MFMA, KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_helper_xof", "k_jr", "k_flp_weights", "k_flp_query",
@@ -151,7 +152,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
     "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
     "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave", "k_shard_norm",
-    "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols", "k_helper_sponge"};
+    "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols", "k_helper_sponge", "k_flp_wires_mfma"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -209,6 +210,7 @@ struct prio3gpu_ctx {
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   bool wires_cols = true;      // chunk <= 64: k_flp_wires_cols; PRIO3GPU_WIRES_COLS=0: k_flp_wires
+  bool wires_mfma = true;      // SumVec chunk > 64: k_flp_wires_mfma; PRIO3GPU_WIRES_MFMA=0: k_flp_wires
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
@@ -826,6 +828,14 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
       hipLaunchKernelGGL(k_flp_wires_cols, grid1((size_t)N << lg, 256), dim3(256), 0, c->stream, g,
                          N, lg, meas, wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                          Rows{st->prep.u8(), g.prep_share_len}, d_status);
+    } else if (FO::ES == 16 && g.kind == KIND_SUMVEC && g.chunk > 64 && g.calls <= kWmMaxCalls &&
+               c->wires_mfma && wires_mfma_lds(g.calls) <= 64 * 1024 && c->flp_weights_lane) {
+      // byte-limb convolution on v_mfma_i32_32x32x32_i8 (wires_mfma.h): a wave per 32 columns
+      const uint32_t nwv = std::min(4u, (g.chunk + 31) / 32);
+      PROF(KID_FLP_WIRES_MFMA);
+      hipLaunchKernelGGL(k_flp_wires_mfma, dim3(N), dim3(64 * nwv), wires_mfma_lds(g.calls),
+                         c->stream, g, N, meas, wrows, Rows{st->prep.u8(), g.prep_share_len},
+                         d_status);
     } else {
       PROF(KID_FLP_WIRES);
       hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
@@ -1140,6 +1150,7 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   }
   if (const char* fq = getenv("PRIO3GPU_FLPQ_BLOCK")) c->flp_query_lane = fq[0] == '0';
   if (const char* wc = getenv("PRIO3GPU_WIRES_COLS")) c->wires_cols = wc[0] != '0';
+  if (const char* wm = getenv("PRIO3GPU_WIRES_MFMA")) c->wires_mfma = wm[0] != '0';
   if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
     const long v = strtol(ws, nullptr, 10);

@@ -782,7 +782,9 @@ struct FlpDims {
 
 // W row written by k_flp_query in split mode (ParallelSum types) and read by k_flp_wires:
 //   MM[1..calls] | LM[1..calls] | RP[1..c] | B0[c] = L0 s_2j | B1[c] = L0 s_2j+1 - (1/2) sum L_k | gsum
-__host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + 3 * cfg.chunk + 1; }
+// (k_flp_weights also appends SMM = sum_k MM[k] and SLM = sum_k LM[k] mod p: k_flp_wires_mfma's
+// offset correction, wires_mfma.h)
+__host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + 3 * cfg.chunk + 3; }
 
 template <class FO>
 __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
@@ -1633,6 +1635,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   }
   // MM[k] = LM[k] rc^(k-1)
   T q = one;
+  T smm = FO::zero();
   for (uint32_t k0 = 1; k0 <= C; k0 += kFwChunk) {
     T vb[kFwChunk];
 #pragma unroll
@@ -1642,6 +1645,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
     for (uint32_t u = 0; u < kFwChunk; ++u) {
       if (k0 + u <= C) {
         vb[u] = FO::mul(vb[u], q);
+        smm = FO::add(smm, vb[u]);
         q = FO::mul(q, rp);
       }
     }
@@ -1735,6 +1739,8 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   const T gsum = wide_reduce(gw);
   if (!live) return;
   FO::store(wm.el(rr, 2 * C + 3 * c), gsum);
+  FO::store(wm.el(rr, 2 * C + 3 * c + 1), smm);
+  FO::store(wm.el(rr, 2 * C + 3 * c + 2), lsum);
   uint8_t* outp = out_prep.at(rr);
   if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
   FO::store(outp + (size_t)(1 + arity) * 16, pt);

@@ -1,0 +1,257 @@
+// FLP wire pass for ParallelSum(Mul) (SumVec, chunk > 64) on the matrix cores.
+//
+// Same outputs as k_flp_wires (prio3_kernels.h), i.e. the query side of prio 0.15.1's
+// ParallelSum(Mul) gadget wires that Janus reaches through Prio3::prepare_init
+// (aggregator/src/aggregator.rs:1777-1786; leader: aggregation_job_driver.rs:362-380):
+//   a_j = REDC( sum_k MM[k] x_(k c + j) ),   b_j = REDC( sum_k LM[k] x_(k c + j) )
+//   wire_2j = B0[j] + RP[j] a_j,              wire_2j+1 = B1[j] + b_j
+// with the weights MM, LM (Montgomery form, < p) from k_flp_weights.
+//
+// The Field128 products are computed EXACTLY as integers by byte-limb convolution on
+// v_mfma_i32_32x32x32_i8 instead of 2 x 16 v_mad_u64_u32 per element on the VALU:
+//   * x (measurement share element, 16 canonical bytes) enters as x' = x - K128 with
+//     K128 = 0x8080...80: byte-wise x'_a = x_a ^ 0x80 in [-128, 127] (4 v_xor per element);
+//   * a weight w enters as 17 signed digits d_b in [-128, 127] (w + K128, bytes ^ 0x80, the carry
+//     out as d_16), converted once per report into LDS;
+//   * for call k the A operand is the 32 x 16 Toeplitz matrix T_k[s][a] = d_(k, s-a), the B
+//     operand the 16 bytes of x'_(k, j) for 32 columns j, so one MFMA (K = 32 = two calls)
+//     accumulates acc[s][j] += sum_(a+b=s) x'_(k,j,a) d_(k,b) for s = 0..31;
+//   * sum_s acc[s][j] 2^(8s) = sum_k w_k x'_(k,j) exactly (|acc| <= calls 2^18 < 2^31), and
+//     adding K128 * sum_k w_k gives sum_k w_k x_(k,j), REDC'd by wide_reduce like the VALU path
+//     (sum_k w_k enters as (its value mod p, from k_flp_weights) + calls p: same residue, and
+//     never below the integer sum, so the total stays non-negative).
+// Every A/B element pair the hardware multiplies shares its K index by construction, so the
+// result does not depend on the i8 operand's k order; the C/D map is the documented one
+// (col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)).
+//
+// Shape: block per report, wave per 32-column tile (up to 4 waves, then tiles loop; chunk 89:
+// 3 waves), lane (n = lane & 31,
+// h = lane >> 5) loads element (2q + h, 32 t + n) at K-step q: each half-wave reads 512
+// contiguous bytes per K-step, every element exactly once.  The VALU keeps 4 xors, a compare and
+// the Toeplitz fragment (5 LDS dwords + 4 v_alignbit, per wire) per element pair; the MFMA work
+// (2 x 32 cycles per K-step per wave) is far below the HBM time.
+#pragma once
+#include "field.h"
+#include "wide.h"
+
+namespace p3g {
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x16_t __attribute__((ext_vector_type(16)));
+
+// timing-only diagnostic build (wrong bytes): no main loop
+#ifndef WM_DIAG_NOLOOP
+#define WM_DIAG_NOLOOP 0
+#endif
+#ifndef WM_U
+#define WM_U 4  // K-steps whose loads are issued together
+#endif
+constexpr uint32_t kWmEDwords = 12;     // 48-byte reversed digit window per (call, wire)
+constexpr uint32_t kWmMaxCalls = 8000;  // |acc| <= calls * 16 * 2^14 < 2^31
+
+__host__ __device__ inline size_t wires_mfma_lds(uint32_t calls) {
+  const size_t kq = (calls + 1) / 2;
+  return (size_t)(2 * kq) * 2 * kWmEDwords * 4 + 16;
+}
+
+
+
+DEVI uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m), hi = __shfl_xor((uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRows meas, WMat wm,
+                                                         Rows out_prep, uint8_t* status) {
+  using FO = Field128Ops;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t r = blockIdx.x;
+  if (r >= n) return;
+  if (status[r] != ST_OK) return;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x, nw = nthr >> 6;
+  const uint32_t wave = tid >> 6, lane = tid & 63u;
+  const uint32_t C = cfg.calls, c = cfg.chunk, KQ = (C + 1) / 2;
+  uint32_t* E = reinterpret_cast<uint32_t*>(smem);        // [2 KQ calls][2 wires][12 dwords]
+  uint32_t* flag = E + (size_t)(2 * KQ) * 2 * kWmEDwords;
+  if (tid == 0) *flag = 0u;
+
+  // ---- weights -> signed byte digits (reversed, zero-padded windows) ----
+  for (uint32_t k = tid; k < 2 * KQ; k += nthr) {
+#pragma unroll
+    for (uint32_t w = 0; w < 2; ++w) {
+      F128 x = FO::zero();
+      if (k < C) x = FO::load(wm.el(r, w * C + k));
+      // y = x + K128; digits d_b = y_b - 128 (b < 16), d_16 = carry out
+      uint32_t D[4], cy = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t s = (uint64_t)x.w[q] + 0x80808080u + cy;
+        D[q] = (uint32_t)s ^ 0x80808080u;
+        cy = (uint32_t)(s >> 32);
+      }
+      uint4* row = reinterpret_cast<uint4*>(E + ((size_t)k * 2 + w) * kWmEDwords);
+      // E[m] = d_(31 - m): bytes 15..31 hold d_16..d_0, the rest zero
+      row[0] = make_uint4(0u, 0u, 0u, cy << 24);
+      row[1] = make_uint4(__builtin_bswap32(D[3]), __builtin_bswap32(D[2]),
+                          __builtin_bswap32(D[1]), __builtin_bswap32(D[0]));
+      row[2] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __syncthreads();
+
+  // ---- main loop: wave = 32-column tile, K-step q covers calls 2q (h = 0) and 2q + 1 (h = 1) ----
+  const uint32_t nn = lane & 31u, h = lane >> 5;
+  const uint32_t o = 31u - nn;  // A row s = nn: the fragment is E[o .. o + 15]
+  const uint32_t sh = 8u * (o & 3u);
+  const uint32_t* Eh = E + (size_t)h * 2 * kWmEDwords + (o >> 2);
+  const uint8_t* xr = meas.at(r);
+  const uint32_t ML = cfg.meas_len;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)xr, (short)0, ML * 16u, kBufRsrcWord3);
+  const uint32_t NT = (c + 31u) / 32u;
+  bool bad = false;
+  for (uint32_t tile = wave; tile < NT; tile += nw) {  // 32-column tiles
+    const uint32_t j = tile * 32u + nn;
+    const bool colok = j < c;
+    i32x16_t acc_a, acc_b;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc_a[i] = 0;
+      acc_b[i] = 0;
+    }
+    uint64_t maybe = 0ull;  // lane mask: some element with top word 2^32 - 1 (exact check below)
+    constexpr uint32_t U = WM_U;
+    for (uint32_t q0 = 0; q0 < (WM_DIAG_NOLOOP ? 0u : KQ); q0 += U) {
+      uint4 xv[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        // raw buffer loads: a dead slot (padding, column >= chunk) gets an offset past the row and
+        // reads zero, so no branch (a branch around each load made the compiler wait for every
+        // load before issuing the next)
+        const uint32_t idx = (2 * (q0 + u) + h) * c + j;
+        const bool v = colok && idx < ML && q0 + u < KQ;
+        const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, v ? idx * 16u : 0xFFFFFFF0u, 0, 0);
+        xv[u] = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        if (q0 + u < KQ) {
+          maybe |= __ballot(xv[u].w == 0xFFFFFFFFu);
+          const i32x4_t b = {(int)(xv[u].x ^ 0x80808080u), (int)(xv[u].y ^ 0x80808080u),
+                             (int)(xv[u].z ^ 0x80808080u), (int)(xv[u].w ^ 0x80808080u)};
+          const uint32_t* ea = Eh + (size_t)(q0 + u) * 4 * kWmEDwords;
+          const uint32_t* eb = ea + kWmEDwords;
+          const i32x4_t fa = {(int)__builtin_amdgcn_alignbit(ea[1], ea[0], sh),
+                              (int)__builtin_amdgcn_alignbit(ea[2], ea[1], sh),
+                              (int)__builtin_amdgcn_alignbit(ea[3], ea[2], sh),
+                              (int)__builtin_amdgcn_alignbit(ea[4], ea[3], sh)};
+          const i32x4_t fb = {(int)__builtin_amdgcn_alignbit(eb[1], eb[0], sh),
+                              (int)__builtin_amdgcn_alignbit(eb[2], eb[1], sh),
+                              (int)__builtin_amdgcn_alignbit(eb[3], eb[2], sh),
+                              (int)__builtin_amdgcn_alignbit(eb[4], eb[3], sh)};
+          acc_a = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, b, acc_a, 0, 0, 0);
+          acc_b = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb, b, acc_b, 0, 0, 0);
+        }
+      }
+    }
+    if (maybe) {  // rare: exact canonical check over this lane's elements
+      for (uint32_t q = 0; q < KQ; ++q) {
+        const uint32_t idx = (2 * q + h) * c + j;
+        if (colok && idx < ML) bad |= !FO::is_canonical(FO::load(xr + (size_t)idx * 16));
+      }
+    }
+
+    // ---- epilogue: lane h finishes wire h of column j ----
+    // Lane half h holds rows 8g + 4h + i (g, i < 4) = bytes 4i of 32-bit word 2g + h.
+    int64_t gown[4], goth[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      int64_t va = 0, vb = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        va += (int64_t)acc_a[4 * g + i] << (8 * i);
+        vb += (int64_t)acc_b[4 * g + i] << (8 * i);
+      }
+      gown[g] = h ? vb : va;
+      goth[g] = h ? va : vb;
+    }
+    int64_t T[8];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int64_t rv = (int64_t)shfl_xor_u64((uint64_t)goth[g], 32);
+      T[2 * g] = h ? rv : gown[g];
+      T[2 * g + 1] = h ? gown[g] : rv;
+    }
+    uint32_t S[10];
+    {
+      int64_t cr = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        const int64_t v = T[w] + cr;
+        S[w] = (uint32_t)v;
+        cr = v >> 32;
+      }
+      S[8] = (uint32_t)cr;
+      S[9] = (uint32_t)(cr >> 32);
+    }
+    // + K128 * W', W' = (sum_k w_k mod p) + calls p >= sum_k w_k (the integer), so the total stays
+    // >= 0 and == sum_k w_k x_k (mod p); the sums come from k_flp_weights (SMM, SLM)
+    {
+      const F128 wsum = FO::load(wm.el(r, 2 * C + 3 * c + 1 + h));
+      uint32_t Wd[6];
+      {
+        const int64_t CC = (int64_t)C;
+        const int64_t v[5] = {(int64_t)wsum.w[0] + CC, (int64_t)wsum.w[1],
+                              (int64_t)wsum.w[2] - 28 * CC, (int64_t)wsum.w[3], CC};
+        int64_t cr = 0;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          const int64_t t = v[q] + cr;
+          Wd[q] = (uint32_t)t;
+          cr = t >> 32;
+        }
+        Wd[5] = (uint32_t)cr;
+      }
+      uint32_t M[7];
+      uint64_t mc = 0;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const uint64_t v = (uint64_t)Wd[q] * 0x80808080u + mc;
+        M[q] = (uint32_t)v;
+        mc = v >> 32;
+      }
+      M[6] = (uint32_t)mc;
+      uint64_t sc = 0;
+#pragma unroll
+      for (int w = 0; w < 10; ++w) {
+        uint64_t v = (uint64_t)S[w] + sc;
+#pragma unroll
+        for (int sft = 0; sft < 4; ++sft)
+          if (w - sft >= 0 && w - sft < 7) v += M[w - sft];
+        S[w] = (uint32_t)v;
+        sc = v >> 32;
+      }
+    }
+    Wide wd;
+    wide_zero(wd);
+#pragma unroll
+    for (int w = 0; w < 6; ++w) wd.lo[w] = S[w];
+    wd.lo[6] = ((uint64_t)S[7] << 32) | S[6];
+    wd.hi[6] = S[8];
+    const F128 v = wide_reduce(wd);
+    if (colok) {
+      uint8_t* outp = out_prep.at(r);
+      if (h == 0) {
+        const F128 rp = FO::load(wm.el(r, 2 * C + j));  // Montgomery
+        FO::store(outp + (size_t)(1 + 2 * j) * 16, FO::add(FO::load(wm.el(r, 2 * C + c + j)), FO::mul(rp, v)));
+      } else {
+        FO::store(outp + (size_t)(2 + 2 * j) * 16, FO::add(FO::load(wm.el(r, 2 * C + 2 * c + j)), v));
+      }
+    }
+  }
+  if (bad) atomicOr(flag, 1u);
+  __syncthreads();
+  if (tid == 0 && (*flag & 1u)) status[r] = ST_INVALID_MESSAGE;
+}
+
+}  // namespace p3g

@@ -28,6 +28,14 @@ CONFIGS = {
                        chunk=3),
     "sumvec_8_1000": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(8, 1000, 89), bits=8,
                           length=1000, chunk=89),
+    # chunk > 64 shapes for k_flp_wires_mfma: an odd number of calls with a padded last call, a
+    # chunk that is a multiple of 32 (no spare column), 65 columns (one in the last tile)
+    "sumvec_odd_calls": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(1, 650, 100), bits=1,
+                             length=650, chunk=100),
+    "sumvec_chunk128": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(1, 1000, 128), bits=1,
+                            length=1000, chunk=128),
+    "sumvec_chunk65": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(3, 300, 65), bits=3,
+                           length=300, chunk=65),
     "hist4": dict(kind=3, ctor=lambda: O.Prio3.new_histogram(4, 2), bits=0, length=4, chunk=2),
     "hist256": dict(kind=3, ctor=lambda: O.Prio3.new_histogram(256, 16), bits=0, length=256,
                     chunk=16),

@@ -13,7 +13,7 @@ from tests.reports import CONFIGS, expected_aggregate, make_batch, plaintext_sum
 pytestmark = pytest.mark.gpu
 
 SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sum5": 24, "sum1": 16, "sum64": 16, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
-         "hist256": 24, "sumvec_8_1000": 6, "fp16_3": 12, "fp32_5": 8, "fp64_4": 8, "fp16_300": 6,
+         "hist256": 24, "sumvec_8_1000": 6, "sumvec_odd_calls": 8, "sumvec_chunk128": 8, "sumvec_chunk65": 8, "fp16_3": 12, "fp32_5": 8, "fp64_4": 8, "fp16_300": 6,
          "fp16_5000": 2}
 FPVEC = [k for k in SIZES if k.startswith("fp")]
 
@@ -150,7 +150,8 @@ def test_noncanonical_leader_share_is_invalid_message():
     assert lst[3] == 8 and (np.delete(lst, 3) == 0).all()
 
 
-@pytest.mark.parametrize("name", ["hist256", "sumvec_small", "countvec15"])
+@pytest.mark.parametrize("name", ["hist256", "sumvec_small", "countvec15", "sumvec_8_1000",
+                                  "sumvec_odd_calls"])
 def test_noncanonical_element_inside_a_lane_group(name):
     """A non-canonical measurement element deep inside the share (not the first element) rejects
     only its report, whichever lane of a multi-report wave (k_flp_wires_cols: G lanes per report)
