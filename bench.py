@@ -40,6 +40,7 @@ METRIC = "reports/sec prepared+aggregated, Prio3SumVec len=1000, 1/2/4/8 GPUs"
 # x 2 (FMA)  ->  int32 VALU 78.6 Tops/s;  HBM3E 8.0 TB/s.
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
+HBM_COPY_GBS = 6290.0  # measured float4 copy (MI355X_MICROARCH.md): the achievable stream rate
 # SURVEY.md §8(d) declared cost model: 7,440 int32 VALU ops per Keccak-f[1600]; 36 per F128 mul.
 OPS_PER_PERM = 7440
 # VALU issue rate: 256 CU x 4 SIMD x 2.4 GHz, a wave64 instruction every 2 cycles on a 32-lane SIMD
@@ -103,15 +104,16 @@ def load_pmc(config):
     return {}
 
 
-def flp_wires_bytes_per_report(s):
-    """Algorithmic HBM bytes of k_flp_wires per report (ParallelSum types): the measurement share
-    once, the weight row W = MM[calls] | LM[calls] | RP[c] | B0[c] | B1[c] | gsum, and the
-    2c wire values written into the prep share."""
+def flp_wires_bytes_per_report(s, mfma=False):
+    """Algorithmic HBM bytes of the FLP wire pass per report (ParallelSum types): the measurement
+    share once, the weight-row entries it reads -- MM[calls] | LM[calls] | RP[c] | B0[c] | B1[c],
+    plus gsum (k_flp_wires) or SMM, SLM (k_flp_wires_mfma) -- and the 2c wire values written into
+    the prep share."""
     es = s.field_size
     arity = s.verifier_len - 2
     c = arity // 2
     calls = -(-s.meas_len // c)
-    w_len = 2 * calls + 3 * c + 1
+    w_len = 2 * calls + 3 * c + (2 if mfma else 1)
     return (s.meas_len + w_len + arity) * es
 
 
@@ -755,15 +757,18 @@ def main():
             if dname in perms and perms[dname]:
                 roof["valu_insts_per_perm"] = round(pm["valu_insts_per_wave"] / perms[dname], 1)
     # the HBM-bound kernel of the step: the FLP wire pass streams each measurement share once
-    hbm_k = "k_flp_wires"
+    hbm_k = "k_flp_wires_mfma" if kt.get("k_flp_wires_mfma", (0, 0))[1] else "k_flp_wires"
     if hbm_k in kt and kt[hbm_k][1]:
         hms, hl = kt[hbm_k]
         h_avg = hms / 1e3 / hl
-        alg = nlaunch * flp_wires_bytes_per_report(s)
+        alg = nlaunch * flp_wires_bytes_per_report(s, hbm_k == "k_flp_wires_mfma")
         hb = {"kernel": hbm_k, "avg_launch_ms": round(h_avg * 1e3, 3),
               "algorithmic_bytes_per_launch": alg,
               "achieved": round(alg / h_avg / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-              "frac": round(alg / h_avg / 1e9 / HBM_PEAK_GBS, 4), "traffic": None}
+              "frac": round(alg / h_avg / 1e9 / HBM_PEAK_GBS, 4),
+              # MI355X_MICROARCH.md: 6.29 TB/s measured for a float4 copy (79 % of the spec)
+              "frac_of_measured_copy": round(alg / h_avg / 1e9 / HBM_COPY_GBS, 4),
+              "traffic": None}
         hp = pmc.get("kernels", {}).get(hbm_k)
         if hp and hp.get("hbm_bytes_per_launch"):
             hb["traffic"] = hp["hbm_bytes_per_launch"]

@@ -43,6 +43,9 @@ typedef int i32x16_t __attribute__((ext_vector_type(16)));
 #ifndef WM_DIAG_NOLOOP
 #define WM_DIAG_NOLOOP 0
 #endif
+#ifndef WM_PREFETCH
+#define WM_PREFETCH 1
+#endif
 #ifndef WM_U
 #define WM_U 4  // K-steps whose loads are issued together
 #endif
@@ -75,6 +78,32 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
   uint32_t* flag = E + (size_t)(2 * KQ) * 2 * kWmEDwords;
   if (tid == 0) *flag = 0u;
 
+  const uint32_t nn = lane & 31u, h = lane >> 5;
+  const uint32_t o = 31u - nn;  // A row s = nn: the fragment is E[o .. o + 15]
+  const uint32_t sh = 8u * (o & 3u);
+  const uint32_t* Eh = E + (size_t)h * 2 * kWmEDwords + (o >> 2);
+  const uint8_t* xr = meas.at(r);
+  const uint32_t ML = cfg.meas_len;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)xr, (short)0, ML * 16u, kBufRsrcWord3);
+  const uint32_t NT = (c + 31u) / 32u;
+  // B fragments of K-steps [q0, q0 + U) of a tile.  Raw buffer loads: a dead slot (padding, column
+  // >= chunk, K-step >= KQ) gets an offset past the row and reads zero, so no branch (a branch
+  // around each load made the compiler wait for every load before issuing the next).
+  constexpr uint32_t U = WM_U;
+  auto load_batch = [&](uint32_t tile, uint32_t q0, uint4* xv) {
+    const uint32_t j = tile * 32u + nn;
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t idx = (2 * (q0 + u) + h) * c + j;
+      const bool v = j < c && idx < ML && q0 + u < KQ;
+      const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, v ? idx * 16u : 0xFFFFFFF0u, 0, 0);
+      xv[u] = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+  };
+  uint4 xv[U];
+  if (WM_PREFETCH) load_batch(wave, 0, xv);  // in flight while the weights are converted
+
   // ---- weights -> signed byte digits (reversed, zero-padded windows) ----
   for (uint32_t k = tid; k < 2 * KQ; k += nthr) {
 #pragma unroll
@@ -100,15 +129,6 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
   __syncthreads();
 
   // ---- main loop: wave = 32-column tile, K-step q covers calls 2q (h = 0) and 2q + 1 (h = 1) ----
-  const uint32_t nn = lane & 31u, h = lane >> 5;
-  const uint32_t o = 31u - nn;  // A row s = nn: the fragment is E[o .. o + 15]
-  const uint32_t sh = 8u * (o & 3u);
-  const uint32_t* Eh = E + (size_t)h * 2 * kWmEDwords + (o >> 2);
-  const uint8_t* xr = meas.at(r);
-  const uint32_t ML = cfg.meas_len;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)xr, (short)0, ML * 16u, kBufRsrcWord3);
-  const uint32_t NT = (c + 31u) / 32u;
   bool bad = false;
   for (uint32_t tile = wave; tile < NT; tile += nw) {  // 32-column tiles
     const uint32_t j = tile * 32u + nn;
@@ -120,19 +140,8 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
       acc_b[i] = 0;
     }
     uint64_t maybe = 0ull;  // lane mask: some element with top word 2^32 - 1 (exact check below)
-    constexpr uint32_t U = WM_U;
     for (uint32_t q0 = 0; q0 < (WM_DIAG_NOLOOP ? 0u : KQ); q0 += U) {
-      uint4 xv[U];
-#pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        // raw buffer loads: a dead slot (padding, column >= chunk) gets an offset past the row and
-        // reads zero, so no branch (a branch around each load made the compiler wait for every
-        // load before issuing the next)
-        const uint32_t idx = (2 * (q0 + u) + h) * c + j;
-        const bool v = colok && idx < ML && q0 + u < KQ;
-        const auto t = __builtin_amdgcn_raw_buffer_load_b128(rs, v ? idx * 16u : 0xFFFFFFF0u, 0, 0);
-        xv[u] = make_uint4(t[0], t[1], t[2], t[3]);
-      }
+      if (!WM_PREFETCH || q0 > 0 || tile != wave) load_batch(tile, q0, xv);
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         if (q0 + u < KQ) {
