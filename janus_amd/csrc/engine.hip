@@ -821,21 +821,31 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
   if (psum) {
     size_t lds2 = esz * (2 * (size_t)g.calls + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
     lds2 = (lds2 + 15) & ~(size_t)15;
-    if (FO::ES == 16 && g.chunk <= 64 && c->wires_cols) {
+    const bool mfma_ok = FO::ES == 16 && c->wires_mfma && c->flp_weights_lane &&
+                         g.calls <= kWmMaxCalls;
+    if (mfma_ok && g.chunk >= 8 && g.chunk <= 32 && 4 * wires_mfma_e_bytes(g.calls) <= 64 * 1024) {
+      // short rows (Histogram): a wave per report on v_mfma_i32_32x32x32_i8 (wires_mfma.h)
+      PROF(KID_FLP_WIRES_MFMA);
+      hipLaunchKernelGGL(k_flp_wires_mfma<true>, grid1(N, 4), dim3(256),
+                         4 * wires_mfma_e_bytes(g.calls), c->stream, g, N, meas, wrows,
+                         CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
+    } else if (FO::ES == 16 && g.chunk <= 64 && c->wires_cols) {
       uint32_t lg = 0;
       while ((1u << lg) < g.chunk) ++lg;
       PROF(KID_FLP_WIRES_COLS);
       hipLaunchKernelGGL(k_flp_wires_cols, grid1((size_t)N << lg, 256), dim3(256), 0, c->stream, g,
                          N, lg, meas, wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                          Rows{st->prep.u8(), g.prep_share_len}, d_status);
-    } else if (FO::ES == 16 && g.kind == KIND_SUMVEC && g.chunk > 64 && g.calls <= kWmMaxCalls &&
-               c->wires_mfma && wires_mfma_lds(g.calls) <= 64 * 1024 && c->flp_weights_lane) {
+    } else if (mfma_ok && g.kind == KIND_SUMVEC && g.chunk > 64 &&
+               wires_mfma_e_bytes(g.calls) + 16 <= 64 * 1024) {
       // byte-limb convolution on v_mfma_i32_32x32x32_i8 (wires_mfma.h): a wave per 32 columns
       const uint32_t nwv = std::min(4u, (g.chunk + 31) / 32);
       PROF(KID_FLP_WIRES_MFMA);
-      hipLaunchKernelGGL(k_flp_wires_mfma, dim3(N), dim3(64 * nwv), wires_mfma_lds(g.calls),
-                         c->stream, g, N, meas, wrows, Rows{st->prep.u8(), g.prep_share_len},
-                         d_status);
+      hipLaunchKernelGGL(k_flp_wires_mfma<false>, dim3(N), dim3(64 * nwv),
+                         wires_mfma_e_bytes(g.calls) + 16, c->stream, g, N, meas, wrows,
+                         CRows{st->jr.u8(), (size_t)g.jr_len * es},
+                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
     } else {
       PROF(KID_FLP_WIRES);
       hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,

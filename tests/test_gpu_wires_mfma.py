@@ -12,17 +12,23 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 # (bits, length, chunk): calls, columns per last tile
-SHAPES = [(8, 1000, 89),   # 90 calls, last call 79 of 89 columns; 3 tiles, 25 in the last
-          (1, 650, 100),   # 7 calls (odd: a zero-weight padding call), 4 tiles
-          (1, 1000, 128),  # 8 calls, 4 full tiles (no spare column)
-          (3, 300, 65),    # 14 calls, a 1-column last tile
-          (2, 3000, 300)]  # 20 calls, 10 tiles (640 threads)
+# (kind, bits, length, chunk); SumVec = 2, Histogram = 3
+SHAPES = [(2, 8, 1000, 89),   # 90 calls, last call 79 of 89 columns; 3 tiles, 25 in the last
+          (2, 1, 650, 100),   # 7 calls (odd: a zero-weight padding call), 4 tiles
+          (2, 1, 1000, 128),  # 8 calls, 4 full tiles (no spare column)
+          (2, 3, 300, 65),    # 14 calls, a 1-column last tile
+          (2, 2, 3000, 300),  # 20 calls, 10 tiles, 4 waves looping over them
+          # short rows (chunk 8..32): a wave per report, 4 reports per block
+          (3, 0, 256, 16),    # Histogram256 (BASELINE config C): 16 calls; v needs sum x
+          (3, 0, 100, 10),    # Histogram, 10 calls
+          (2, 4, 100, 32),    # 13 calls (odd), a full 32-column tile
+          (2, 1, 300, 24)]    # 13 calls, padding in the last call
 
 
-def _vdaf(bits, length, chunk, monkeypatch, mfma, vk=bytes(range(16))):
-    from janus_amd.prio3 import SUMVEC, Prio3Gpu
+def _vdaf(kind, bits, length, chunk, monkeypatch, mfma, vk=bytes(range(16))):
+    from janus_amd.prio3 import Prio3Gpu
     monkeypatch.setenv("PRIO3GPU_WIRES_MFMA", "1" if mfma else "0")
-    return Prio3Gpu(SUMVEC, vk, bits=bits, length=length, chunk_length=chunk)
+    return Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk)
 
 
 def _random_shares(rng, n, s, meas_len, extremes):
@@ -39,14 +45,16 @@ def _random_shares(rng, n, s, meas_len, extremes):
     return lin
 
 
-@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "sumvec_%d_%d_%d" % s)
+@pytest.mark.parametrize("shape", SHAPES,
+                         ids=lambda s: ("sumvec_%d_%d_%d" % s[1:]) if s[0] == 2 else
+                         "histogram_%d_%d" % s[2:])
 def test_mfma_wires_match_valu(shape, monkeypatch):
-    bits, length, chunk = shape
+    kind, bits, length, chunk = shape
     rng = np.random.default_rng(chunk)
-    vm = _vdaf(bits, length, chunk, monkeypatch, True)
-    vv = _vdaf(bits, length, chunk, monkeypatch, False)
+    vm = _vdaf(kind, bits, length, chunk, monkeypatch, True)
+    vv = _vdaf(kind, bits, length, chunk, monkeypatch, False)
     s = vm.sizes
-    meas_len = bits * length
+    meas_len = bits * length if kind == 2 else length
     n = 640
     nonces = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
     pub = rng.integers(0, 256, size=(n, s.public_share), dtype=np.uint8)
@@ -77,7 +85,7 @@ def test_mfma_wires_helper_path(monkeypatch):
     b = make_batch("sumvec_8_1000", 6)
     out = []
     for mfma in (True, False):
-        v = _vdaf(8, 1000, 89, monkeypatch, mfma, b.verify_key)
+        v = _vdaf(2, 8, 1000, 89, monkeypatch, mfma, b.verify_key)
         hs = v.new_state(1, b.n)
         agg = v.new_aggregate(1)
         msgs, st = v.helper_init(hs, b.nonces, b.public, b.helper_in, b.leader_prep, agg=agg)
