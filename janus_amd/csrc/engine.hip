@@ -211,6 +211,8 @@ struct prio3gpu_ctx {
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   bool wires_cols = true;      // chunk <= 64: k_flp_wires_cols; PRIO3GPU_WIRES_COLS=0: k_flp_wires
   bool wires_mfma = true;      // SumVec chunk > 64: k_flp_wires_mfma; PRIO3GPU_WIRES_MFMA=0: k_flp_wires
+  bool wires_mfma_short = false;  // chunk 8..32 (Histogram): k_flp_wires_mfma<SHORT>; opt-in
+                                  // until measured (PRIO3GPU_WIRES_MFMA_SHORT=1)
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
   size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
@@ -823,7 +825,8 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
     lds2 = (lds2 + 15) & ~(size_t)15;
     const bool mfma_ok = FO::ES == 16 && c->wires_mfma && c->flp_weights_lane &&
                          g.calls <= kWmMaxCalls;
-    if (mfma_ok && g.chunk >= 8 && g.chunk <= 32 && 4 * wires_mfma_e_bytes(g.calls) <= 64 * 1024) {
+    if (mfma_ok && c->wires_mfma_short && g.chunk >= 8 && g.chunk <= 32 &&
+        4 * wires_mfma_e_bytes(g.calls) <= 64 * 1024) {
       // short rows (Histogram): a wave per report on v_mfma_i32_32x32x32_i8 (wires_mfma.h)
       PROF(KID_FLP_WIRES_MFMA);
       hipLaunchKernelGGL(k_flp_wires_mfma<true>, grid1(N, 4), dim3(256),
@@ -1161,6 +1164,7 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   if (const char* fq = getenv("PRIO3GPU_FLPQ_BLOCK")) c->flp_query_lane = fq[0] == '0';
   if (const char* wc = getenv("PRIO3GPU_WIRES_COLS")) c->wires_cols = wc[0] != '0';
   if (const char* wm = getenv("PRIO3GPU_WIRES_MFMA")) c->wires_mfma = wm[0] != '0';
+  if (const char* ws = getenv("PRIO3GPU_WIRES_MFMA_SHORT")) c->wires_mfma_short = ws[0] == '1';
   if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
     const long v = strtol(ws, nullptr, 10);

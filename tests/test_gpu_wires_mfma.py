@@ -28,6 +28,7 @@ SHAPES = [(2, 8, 1000, 89),   # 90 calls, last call 79 of 89 columns; 3 tiles, 2
 def _vdaf(kind, bits, length, chunk, monkeypatch, mfma, vk=bytes(range(16))):
     from janus_amd.prio3 import Prio3Gpu
     monkeypatch.setenv("PRIO3GPU_WIRES_MFMA", "1" if mfma else "0")
+    monkeypatch.setenv("PRIO3GPU_WIRES_MFMA_SHORT", "1" if mfma else "0")
     return Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk)
 
 
