@@ -210,6 +210,7 @@ struct prio3gpu_ctx {
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   bool wires_cols = true;      // chunk <= 64: k_flp_wires_cols; PRIO3GPU_WIRES_COLS=0: k_flp_wires
+  size_t expand_lds = 0;       // PRIO3GPU_EXPAND_LDS: k_expand occupancy cap (A/B)
   bool wires_mfma = true;      // SumVec chunk > 64: k_flp_wires_mfma; PRIO3GPU_WIRES_MFMA=0: k_flp_wires
   bool wires_mfma_short = false;  // chunk 8..32 (Histogram): k_flp_wires_mfma<SHORT>; opt-in
                                   // until measured (PRIO3GPU_WIRES_MFMA_SHORT=1)
@@ -692,7 +693,9 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     }
     {
       PROF(KID_EXPAND);
-      hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N,
+      // c->expand_lds (PRIO3GPU_EXPAND_LDS, A/B knob): unused dynamic LDS that caps the blocks
+      // per CU, i.e. k_expand's occupancy
+      hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), c->expand_lds, c->stream, g, N,
                          (uint32_t)st->agg_id, CRows{d_in, in_pitch}, mo, po, d_status, gate);
     }
     meas = CRows{mo.base, mo.stride};
@@ -1164,6 +1167,8 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   if (const char* fq = getenv("PRIO3GPU_FLPQ_BLOCK")) c->flp_query_lane = fq[0] == '0';
   if (const char* wc = getenv("PRIO3GPU_WIRES_COLS")) c->wires_cols = wc[0] != '0';
   if (const char* wm = getenv("PRIO3GPU_WIRES_MFMA")) c->wires_mfma = wm[0] != '0';
+  if (const char* el = getenv("PRIO3GPU_EXPAND_LDS"))
+    c->expand_lds = std::min<size_t>(strtoull(el, nullptr, 10), 64 * 1024);
   if (const char* ws = getenv("PRIO3GPU_WIRES_MFMA_SHORT")) c->wires_mfma_short = ws[0] == '1';
   if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
   if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {

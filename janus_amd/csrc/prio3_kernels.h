@@ -380,7 +380,10 @@ __global__ void __launch_bounds__(256) k_query_rand(Cfg cfg, uint32_t n, uint64_
 template <class FO>
 // `gate` (optional): run only if *gate != 0 -- the exact path behind k_helper_sponge, which sets
 // it when a lane met a non-canonical element.
-__global__ void __launch_bounds__(256) k_expand(Cfg cfg, uint32_t n, uint32_t agg_id,
+#ifndef P3G_EXPAND_WAVES  // min waves per SIMD for k_expand (A/B knob; 0 = compiler's choice)
+#define P3G_EXPAND_WAVES 0
+#endif
+__global__ void __launch_bounds__(256, P3G_EXPAND_WAVES) k_expand(Cfg cfg, uint32_t n, uint32_t agg_id,
                                                 CRows helper_shares, Rows out_meas,
                                                 Rows out_proof, const uint8_t* status,
                                                 const uint32_t* gate) {
