@@ -210,6 +210,7 @@ struct prio3gpu_ctx {
   bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
   uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
   bool wires_cols = true;      // chunk <= 64: k_flp_wires_cols; PRIO3GPU_WIRES_COLS=0: k_flp_wires
+  bool wrow_align = false;     // PRIO3GPU_WROW_ALIGN=1: weight rows at a 128-B pitch (A/B)
   size_t expand_lds = 0;       // PRIO3GPU_EXPAND_LDS: k_expand occupancy cap (A/B)
   bool wires_mfma = true;      // SumVec chunk > 64: k_flp_wires_mfma; PRIO3GPU_WIRES_MFMA=0: k_flp_wires
   bool wires_mfma_short = false;  // chunk 8..32 (Histogram): k_flp_wires_mfma<SHORT>; opt-in
@@ -797,8 +798,8 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
   }
   // weight rows (row-major), then k_flp_weights' element-major scratch (calls x n entries)
   WMat wrows{nullptr, 0, 0};
-  if (psum) wrows = WMat{st->w.u8(), (size_t)flp_w_len(g) * es, (size_t)es};
-  uint8_t* wscr = psum ? st->w.u8() + (size_t)N * flp_w_len(g) * es : nullptr;
+  if (psum) wrows = WMat{st->w.u8(), (size_t)flp_w_pitch(g, c->wrow_align) * es, (size_t)es};
+  uint8_t* wscr = psum ? st->w.u8() + (size_t)N * flp_w_pitch(g, c->wrow_align) * es : nullptr;
   if (psum && FO::ES == 16 && c->flp_weights_lane) {
     PROF(KID_FLP_WEIGHTS);
     hipLaunchKernelGGL(k_flp_weights, grid1(n, kFwThreads), dim3(kFwThreads), 0, c->stream, g, N,
@@ -1167,6 +1168,7 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   if (const char* fq = getenv("PRIO3GPU_FLPQ_BLOCK")) c->flp_query_lane = fq[0] == '0';
   if (const char* wc = getenv("PRIO3GPU_WIRES_COLS")) c->wires_cols = wc[0] != '0';
   if (const char* wm = getenv("PRIO3GPU_WIRES_MFMA")) c->wires_mfma = wm[0] != '0';
+  if (const char* wa = getenv("PRIO3GPU_WROW_ALIGN")) c->wrow_align = wa[0] == '1';
   if (const char* el = getenv("PRIO3GPU_EXPAND_LDS"))
     c->expand_lds = std::min<size_t>(strtoull(el, nullptr, 10), 64 * 1024);
   if (const char* ws = getenv("PRIO3GPU_WIRES_MFMA_SHORT")) c->wires_mfma_short = ws[0] == '1';
@@ -1278,7 +1280,7 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   rc |= st->msg.ensure(N * 16);
   rc |= st->status.ensure(N);
   if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM)
-    rc |= st->w.ensure(N * (size_t)(flp_w_len(g) + g.calls) * g.es);  // rows + weights scratch
+    rc |= st->w.ensure(N * (size_t)(flp_w_pitch(g, true) + g.calls) * g.es);  // rows + scratch
   if (g.kind == KIND_FPVEC) {
     rc |= st->w.ensure(N * (size_t)fpv_w_layout(g).len * 16);
     rc |= st->fpart.ensure(N * (size_t)fpv_rows(g) * g.chunk * 32);

@@ -788,6 +788,11 @@ struct FlpDims {
 // (k_flp_weights also appends SMM = sum_k MM[k] and SLM = sum_k LM[k] mod p: k_flp_wires_mfma's
 // offset correction, wires_mfma.h)
 __host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + 3 * cfg.chunk + 3; }
+// row pitch in elements: packed, or rounded up to 128 B (8 Field128 / 16 Field64 elements)
+__host__ __device__ inline uint32_t flp_w_pitch(const Cfg& cfg, bool align128) {
+  const uint32_t q = 128u / cfg.es;
+  return align128 ? (flp_w_len(cfg) + q - 1) / q * q : flp_w_len(cfg);
+}
 
 template <class FO>
 __global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
