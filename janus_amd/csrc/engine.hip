@@ -115,10 +115,14 @@ uint32_t ilog2(uint32_t x) {
   return l;
 }
 
-// Grow-only device buffer.
+// Grow-only device buffer; owns its allocation (freed on destruction, never copied).
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   int ensure(size_t bytes) {
     if (bytes <= cap) return 0;
     if (p) HIPCHK(hipFree(p));
@@ -227,6 +231,7 @@ struct prio3gpu_ctx {
   int ev_next = 0;
   uint32_t gen_next = 1;
   hipEvent_t wait_ev = nullptr;  // prio3gpu_ctx_wait: recorded on the other context, not a mark
+  int wait_ev_dev = -1;          // device wait_ev was created on (the other context's)
   std::mutex mark_mu;            // ev_next / ev_gen / wait_ev
   // the device-side accumulation plan of the last call (single slot, no per-report slots):
   // reused while (n, speculative layout, slot count) are unchanged -- no host planning, no upload
@@ -289,7 +294,14 @@ struct prio3gpu_agg {
 struct prio3gpu_comm {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0, device = 0;
+  // all-gather scratch, shared by every context that flushes through this communicator
   DevBuf gather, cgather, mgather;
+  // Flushes through one communicator are serialised: the host issues one at a time (mu), and each
+  // flush's collectives wait on `done`, recorded after the previous flush's k_merge_ranks, so an
+  // async context's collectives never overwrite scratch another context's merge still reads.
+  std::mutex mu;
+  hipEvent_t done = nullptr;
+  bool done_valid = false;
 };
 
 namespace {
@@ -1639,12 +1651,22 @@ int prio3gpu_ctx_wait(prio3gpu_ctx* c, prio3gpu_ctx* other) {
     return PRIO3GPU_E_ARG;
   }
   if (c == other) return 0;
-  HIPCHK(hipSetDevice(c->device));
   // a private event of the waiting context, recorded on the other stream: the other context's
-  // mark ring (marks its caller may still hold) is not touched
+  // mark ring (marks its caller may still hold) is not touched.  An event can only be recorded on
+  // a stream of its own device, so it lives on the other context's device (re-created when the
+  // other context sits on a different device than last time); the wait itself works across devices.
   std::lock_guard<std::mutex> lk(c->mark_mu);
-  if (!c->wait_ev) HIPCHK(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
+  if (c->wait_ev && c->wait_ev_dev != other->device) {
+    (void)hipEventDestroy(c->wait_ev);
+    c->wait_ev = nullptr;
+  }
+  HIPCHK(hipSetDevice(other->device));
+  if (!c->wait_ev) {
+    HIPCHK(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
+    c->wait_ev_dev = other->device;
+  }
   HIPCHK(hipEventRecord(c->wait_ev, other->stream));
+  HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamWaitEvent(c->stream, c->wait_ev, 0));
   return 0;
 }
@@ -1942,9 +1964,15 @@ int prio3gpu_comm_init(const uint8_t id[128], int nranks, int rank, int device,
   cm->nranks = nranks;
   cm->rank = rank;
   cm->device = device;
+  if (hipEventCreateWithFlags(&cm->done, hipEventDisableTiming) != hipSuccess) {
+    set_err("hipEventCreate failed");
+    delete cm;
+    return PRIO3GPU_E_HIP;
+  }
   ncclResult_t e = ncclCommInitRank(&cm->comm, nranks, uid, rank);
   if (e != ncclSuccess) {
     set_err("ncclCommInitRank: %s", ncclGetErrorString(e));
+    (void)hipEventDestroy(cm->done);
     delete cm;
     return PRIO3GPU_E_RCCL;
   }
@@ -1954,8 +1982,15 @@ int prio3gpu_comm_init(const uint8_t id[128], int nranks, int rank, int device,
 
 int prio3gpu_comm_destroy(prio3gpu_comm* cm) {
   if (!cm) return 0;
+  (void)hipSetDevice(cm->device);
+  {
+    std::lock_guard<std::mutex> lk(cm->mu);
+    if (cm->done_valid) (void)hipEventSynchronize(cm->done);  // the last merge has read the scratch
+  }
   cm->gather.release();
   cm->cgather.release();
+  cm->mgather.release();
+  if (cm->done) (void)hipEventDestroy(cm->done);
   if (cm->comm) ncclCommDestroy(cm->comm);
   delete cm;
   return 0;
@@ -1968,7 +2003,14 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
     set_err("bad argument");
     return PRIO3GPU_E_ARG;
   }
+  if (c->device != cm->device) {
+    set_err("context on device %d, communicator on device %d", c->device, cm->device);
+    return PRIO3GPU_E_ARG;
+  }
   HIPCHK(hipSetDevice(c->device));
+  std::lock_guard<std::mutex> lk(cm->mu);
+  // the previous flush (any context) must have finished reading the shared scratch
+  if (cm->done_valid) HIPCHK(hipStreamWaitEvent(c->stream, cm->done, 0));
   const size_t nel = (size_t)local->slots * c->cfg.out_len;
   const size_t bytes = nel * c->cfg.es;
   CHK(cm->gather.ensure(bytes * cm->nranks));
@@ -2007,6 +2049,8 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
                          reinterpret_cast<const SlotMeta*>(cm->mgather.p), local->slots, nb);
   }
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(cm->done, c->stream));
+  cm->done_valid = true;
   if (total) {  // the local partial has been merged: reset it for the next job (flush semantics)
     HIPCHK(hipMemsetAsync(local->share.p, 0, bytes, c->stream));
     HIPCHK(hipMemsetAsync(local->counts.p, 0, (size_t)local->slots * 8, c->stream));

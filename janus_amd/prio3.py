@@ -97,14 +97,19 @@ def _ptr(a) -> Optional[int]:
 def _pitched_rows(a, n: int, width: int, what: str):
     """(buffer, row pitch) of an (n, width) uint8 view whose rows may sit `pitch` >= width bytes
     apart (a column slice of a wider, e.g. 128-B-aligned, buffer: numpy or torch, host or
-    device); anything else goes through `_as_u8` and is packed (pitch = width)."""
+    device).  Only a positive pitch >= width that is a multiple of 16 (what
+    prio3gpu_state_set_input_pitch accepts) is passed through; any other layout -- broadcast
+    (stride 0), negative or unaligned strides, non-contiguous rows -- is packed (pitch = width)."""
     shp = getattr(a, "shape", None)
     if shp is not None and len(shp) == 2 and tuple(shp) == (n, width) and n > 1:
+        pitch = None
         if isinstance(a, np.ndarray) and a.dtype == np.uint8 and a.strides[1] == 1:
-            return a, a.strides[0]
-        if hasattr(a, "data_ptr") and getattr(a, "element_size", lambda: 0)() == 1 and \
+            pitch = a.strides[0]
+        elif hasattr(a, "data_ptr") and getattr(a, "element_size", lambda: 0)() == 1 and \
                 a.stride(1) == 1:
-            return a, a.stride(0)
+            pitch = a.stride(0)
+        if pitch is not None and pitch >= width and (pitch == width or pitch % 16 == 0):
+            return a, pitch
     return _as_u8(a, n, width, what), width
 
 
@@ -134,6 +139,8 @@ def _as_u8(a, n: int, width: int, what: str):
         raise ValueError(f"{what}: expected {n}x{width} bytes, got {_nbytes(a)}")
     if isinstance(a, np.ndarray):
         a = np.ascontiguousarray(a, dtype=np.uint8)
+    elif hasattr(a, "is_contiguous") and not a.is_contiguous():
+        a = a.contiguous()  # torch: packed rows (the engine reads n * width bytes from row 0)
     return a
 
 

@@ -182,3 +182,77 @@ def test_rccl_flush_is_stream_ordered_in_async_mode(with_total):
     if with_total:
         assert local.read(0)[1] == 0 and local.read_reports(0) == (bytes(32), (0, 0))
     comm.close()
+
+
+def test_rccl_flushes_of_two_async_contexts_on_one_comm():
+    """One communicator shared by two async contexts (one comm per process, one
+    context per job worker; Janus runs jobs concurrently, job_driver.rs:119-216).  Both contexts
+    flush different partials back to back with no host wait: the comm's shared all-gather scratch
+    must not be overwritten by the second flush while the first one's k_merge_ranks reads it, so
+    each total equals its own partial (aggregate bytes, count, checksum, interval) -- the
+    BatchAggregation::merged_with of one partial (aggregate_share.rs:47-65)."""
+    import hashlib
+
+    import torch
+    from janus_amd._lib import check, lib
+    from janus_amd.parallel import BatchAggregation, merge_batch_aggregations
+    from janus_amd.prio3 import Comm, Prio3Gpu
+    from tests.reports import CONFIGS, expected_aggregate, make_batch
+    name = "sumvec_small"
+    b = make_batch(name, 48)
+    c = CONFIGS[name]
+    mk = lambda: Prio3Gpu(c["kind"], b.verify_key, bits=c["bits"], length=c["length"],
+                          chunk_length=c["chunk"])
+    ctxs = [mk(), mk()]
+    s = ctxs[0].sizes
+    dev = torch.device("cuda", 0)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    nz, pub, lin, msgs = d(b.nonces), d(b.public), d(b.leader_in), d(b.prep_msg)
+    times = torch.arange(b.n, dtype=torch.int64, device=dev) + 9000
+    lst = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    P = lambda t: t.data_ptr()
+    jobs = [slice(0, 30), slice(30, 48)]
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    states = [v.new_state(0, j.stop - j.start) for v, j in zip(ctxs, jobs)]
+    locals_ = [v.new_aggregate(1) for v in ctxs]
+    totals = [v.new_aggregate(1) for v in ctxs]
+    torch.cuda.synchronize()
+    for rep in range(3):  # repeated: each round flushes into the running totals
+        for v in ctxs:
+            v.set_async(True)
+        for v, st, loc, j in zip(ctxs, states, locals_, jobs):
+            n = j.stop - j.start
+            check(lib().prio3gpu_prepare_init(v._ctx, st._h, n, P(nz[j]), P(pub[j]), P(lin[j]),
+                                              None, P(lst[j])), "prepare_init")
+            check(lib().prio3gpu_prepare_next(v._ctx, st._h, n, P(msgs[j]), P(lst[j]), None, None,
+                                              loc._h), "prepare_next")
+            check(lib().prio3gpu_agg_update_reports(loc._h, n, P(nz[j]), P(times[j]), P(lst[j]),
+                                                    None), "report meta")
+        for v, loc, tot in zip(ctxs, locals_, totals):
+            comm.allreduce(v, loc, tot)  # back to back, queued on two streams, no host wait
+        for v in ctxs:
+            v.sync()
+            v.set_async(False)
+    assert int(lst.max()) == 0
+    for tot, j in zip(totals, jobs):
+        m = np.zeros(b.n, bool)
+        m[j] = True
+        sh, cnt = expected_aggregate(b, "leader", mask=m)
+        # three flushes of the same partial: 3x the share mod p, 3x the count, checksum XOR'd 3x
+        vec = [(3 * x) % ctxs[0].modulus for x in ctxs[0].decode_field_vec(sh)]
+        want = b"".join(int(x).to_bytes(s.field_size, "little") for x in vec)
+        got_sh, got_cnt = tot.read(0)
+        assert got_sh == want and got_cnt == 3 * cnt
+        pck = bytes(32)
+        for i in np.flatnonzero(m):
+            pck = bytes(x ^ y for x, y in zip(pck, hashlib.sha256(b.nonces[i].tobytes()).digest()))
+        ck, iv = tot.read_reports(0)
+        assert ck == pck and iv == (9000 + j.start, j.stop - j.start)
+        one = merge_batch_aggregations(s.field_size, [BatchAggregation(sh, cnt, pck,
+                                                                      (9000 + j.start,
+                                                                       j.stop - j.start))] * 3)
+        assert (one.aggregate_share, one.report_count, one.checksum, one.interval) == \
+            (got_sh, got_cnt, ck, iv)
+    for loc in locals_:
+        assert loc.read(0)[1] == 0
+    comm.close()
