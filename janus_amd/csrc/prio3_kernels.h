@@ -1501,6 +1501,11 @@ __global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights_wave(Cfg cfg, ui
 #ifndef FLPW_M3_SEEDS
 #define FLPW_M3_SEEDS 1
 #endif
+// A/B knob: wave priority (s_setprio) of the FLP query kernels, for schedules that run them beside
+// the sponge kernels of another batch (bench.py --overlap 2); 0 = default priority.
+#ifndef P3G_FLP_PRIO
+#define P3G_FLP_PRIO 0
+#endif
 constexpr uint32_t kFwChunk = 8;                  // elements per LDS window
 constexpr uint32_t kFwWin = 64 * kFwChunk * 16;  // bytes per window (one wave)
 constexpr uint32_t kFwThreads = 128;
@@ -1512,6 +1517,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   using FO = Field128Ops;
   using T = F128;
   __shared__ __attribute__((aligned(16))) uint8_t lds[(kFwThreads / 64) * 2 * kFwWin];
+  if constexpr (P3G_FLP_PRIO > 0) __builtin_amdgcn_s_setprio(P3G_FLP_PRIO);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t r0w = blockIdx.x * blockDim.x + 64u * wv;
   if (r0w >= n) return;  // wave-uniform

@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
   using FO = Field128Ops;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+  if constexpr (P3G_FLP_PRIO > 0) __builtin_amdgcn_s_setprio(P3G_FLP_PRIO);
   const uint32_t r = SHORT ? blockIdx.x * (blockDim.x >> 6) + wave : blockIdx.x;
   if (r >= n) return;  // SHORT: wave-uniform, and nothing below waits for other waves
   if (status[r] != ST_OK) return;

@@ -164,3 +164,75 @@ def test_parser_sees_what_it_should():
     assert h["prio3gpu_last_error"] == (("ptr_const", "c_char"), [])
     assert h["prio3gpu_comm_unique_id"][1] == [("ptr_mut", "u8")]          # out_id[128]
     assert h["prio3gpu_unshard"][1][5] == ("ptr_mut", "f64")
+
+
+MOD = os.path.join(ROOT, "rust", "aggregator", "src", "gpu", "mod.rs")
+BUILD_RS = os.path.join(ROOT, "rust", "aggregator", "build.rs")
+
+
+def _ffi_calls(src):
+    """(name, argument count) of every `ffi::prio3gpu_*(...)` call, arguments split at the
+    call's top-level commas."""
+    src = re.sub(r"//[^\n]*", " ", src)
+    out = []
+    for m in re.finditer(r"ffi::(prio3gpu_\w+)\s*\(", src):
+        i, depth, args, cur = m.end(), 1, [], ""
+        while depth:
+            ch = src[i]
+            if ch in "([{":
+                depth += 1
+            elif ch in ")]}":
+                depth -= 1
+            if depth == 1 and ch == ",":
+                args.append(cur)
+                cur = ""
+            elif depth:
+                cur += ch
+            i += 1
+        if cur.strip():
+            args.append(cur)
+        out.append((m.group(1), len([a for a in args if a.strip()])))
+    return out
+
+
+def test_mod_rs_calls_header_functions_with_their_arity():
+    h = header_functions()
+    calls = _ffi_calls(open(MOD).read())
+    assert len(calls) >= 15
+    for name, n in calls:
+        assert name in h, f"mod.rs calls {name}, which the header does not declare"
+        assert n == len(h[name][1]), f"mod.rs calls {name} with {n} args, header has {len(h[name][1])}"
+
+
+def test_build_rs_keeps_rustc_semver_and_checks_the_hash():
+    """The reference's aggregator/build.rs:3-6 (used by env!("RUSTC_SEMVER"),
+    aggregator/src/metrics.rs:227) stays; the engine build refuses an empty/failed hash."""
+    src = open(BUILD_RS).read()
+    assert "cargo:rustc-env=RUSTC_SEMVER=" in src and "rustc_version::version" in src
+    assert "cargo:rerun-if-env-changed=RUSTC" in src
+    assert "status.success()" in src.split("python3", 1)[1].split("hipcc", 1)[0]
+    assert "len() == 64" in src and "is_ascii_hexdigit" in src
+
+
+def test_every_prio3_vdaf_ops_variant_and_engine_kind_has_an_arm():
+    """GpuVdafOps mirrors the reference's Prio3 VdafOps variants (aggregator.rs:1040-1058) and
+    every `enum prio3gpu_kind` value is reached by some arm."""
+    src = re.sub(r"//[^\n]*", " ", open(MOD).read())
+    enum = re.search(r"pub enum GpuVdafOps \{(.*?)\n\}", src, re.S).group(1)
+    variants = set(re.findall(r"(Prio3\w+)\(", enum))
+    ref = {"Prio3Count", "Prio3CountVec", "Prio3Sum", "Prio3SumVec", "Prio3Histogram",
+           "Prio3FixedPoint16BitBoundedL2VecSum", "Prio3FixedPoint32BitBoundedL2VecSum",
+           "Prio3FixedPoint64BitBoundedL2VecSum"}
+    assert variants == ref
+    kind_fn = re.search(r"pub fn kind\(&self\).*?\n    \}", src, re.S).group(0)
+    for v in ref:
+        assert f"GpuVdafOps::{v}(" in kind_fn, f"kind() has no arm for {v}"
+    hdr = _strip_c_comments(open(HEADER).read())
+    kinds = re.findall(r"(PRIO3GPU_(?:COUNT|SUM|SUMVEC|HISTOGRAM|FPVEC))\s*=", hdr)
+    assert len(kinds) == 5
+    for k in kinds:
+        assert f"ffi::{k}" in kind_fn, f"no GpuVdafOps arm maps to {k}"
+        assert f"ffi::{k}" in re.search(r"pub fn engine_params.*?\n\}", src, re.S).group(0)
+    # leader and helper entry points on every arm (through task())
+    for f in ("helper_aggregate_init", "leader_aggregate_init", "leader_process_response"):
+        assert re.search(rf"impl GpuVdafOps \{{.*pub fn {f}\(", src, re.S), f
