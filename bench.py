@@ -43,6 +43,8 @@ HBM_PEAK_GBS = 8000.0
 HBM_COPY_GBS = 6290.0  # measured float4 copy (MI355X_MICROARCH.md): the achievable stream rate
 # SURVEY.md §8(d) declared cost model: 7,440 int32 VALU ops per Keccak-f[1600]; 36 per F128 mul.
 OPS_PER_PERM = 7440
+OPS_PER_F128_MUL = 36
+OPS_PER_F64_MUL = 10
 # VALU issue rate: 256 CU x 4 SIMD x 2.4 GHz, a wave64 instruction every 2 cycles on a 32-lane SIMD
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 # Measured register-only Keccak-f[1600] ceiling of one MI355X (tools/mb_keccak_occ.hip,
@@ -115,6 +117,24 @@ def flp_wires_bytes_per_report(s, mfma=False):
     calls = -(-s.meas_len // c)
     w_len = 2 * calls + 3 * c + (2 if mfma else 1)
     return (s.meas_len + w_len + arity) * es
+
+
+def flp_mults_per_report(sizes, kind):
+    """SURVEY §8(d)'s FLP op model: field multiplications of ONE aggregator's prio-style FLP query
+    (Type::query with the QueryShim gadget; count the spec algorithm, not this engine's): every
+    wire polynomial interpolated by a size-m inverse NTT (m/2 log2 m) and evaluated at t by
+    Horner (m), the gadget polynomial at t (gp_len), its values at the m-th roots by one
+    size-2m NTT (m log2 2m), and the validity circuit (~2 per measurement element, Count 1).
+    Gives Sum32 ~0.9K, Histogram256 ~4.6K, SumVec(8,1000) ~128K."""
+    arity = sizes.verifier_len - 2
+    calls = {0: 1, 1: sizes.meas_len}.get(kind)
+    if calls is None:  # ParallelSum: chunk = arity / 2 columns per call
+        calls = -(-sizes.meas_len // (arity // 2))
+    m = 1 << max(1, math.ceil(math.log2(calls + 1)))
+    lg = int(math.log2(m))
+    gp_len = sizes.proof_len - arity
+    wires = arity * (m // 2 * lg + m)
+    return wires + gp_len + m * (lg + 1) + (1 if kind == 0 else 2 * sizes.meas_len)
 
 
 def perms_per_report(kind_name, sizes):
@@ -251,6 +271,8 @@ def main():
                     help="N > 1: per-step RCCL all-gather + mod-p merge (the product path), or "
                          "'gloo' = a rehearsal of the multi-rank bench on fewer GPUs than ranks "
                          "(ranks share GPUs, aggregates merged once over gloo at the end)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine option for every context (prio3gpu_ctx_set_option), repeatable")
     ap.add_argument("--workers", type=int, default=1,
                     help="concurrent aggregation-job workers per GPU, one engine context (HIP "
                          "stream) and one contiguous slice of the batch each (Janus "
@@ -307,6 +329,14 @@ def main():
                       xof=xof_id) for _ in range(W)]
     vdaf = vdafs[0]
     s = vdaf.sizes
+    engine_opts = [(o.split("=", 1)[0], int(o.split("=", 1)[1])) for o in args.opt]
+
+    def apply_opts(v):
+        for name, val in engine_opts:
+            v.set_option(name, val)
+        return v
+    for v_ in vdafs:
+        apply_opts(v_)
 
     # ---- synthetic inputs: B distinct reports per rank (SURVEY §8(d) recipe).  The recipe's
     # nonces / client randomness / measurements come from the C restatement (multithreaded); the
@@ -390,8 +420,8 @@ def main():
         wk.n = hi - lo
         # --overlap: the helper gets its own context (HIP stream), so its prepare_init runs
         # concurrently with the leader's, like two aggregator processes sharing the GPU
-        wk.hv = (Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk,
-                          device=gpu, xof=xof_id) if args.overlap else wk.v)
+        wk.hv = (apply_opts(Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk,
+                                     device=gpu, xof=xof_id)) if args.overlap else wk.v)
         wk.ls, wk.hs = wk.v.new_state(0, wk.n), wk.hv.new_state(1, wk.n)
         wk.ls.set_input_pitch(0 if lpitch == s.leader_input_share else lpitch)
         wk.lagg, wk.hagg = wk.v.new_aggregate(1), wk.hv.new_aggregate(1)
@@ -742,6 +772,16 @@ def main():
                     nlaunch * s.meas_len * s.field_size if dname == "k_jr" else
                     nlaunch * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand"
                     else None)}
+    elif dname in ("k_flp_query_lane", "k_flp_query_sum"):  # the whole FLP query of Count / Sum
+        mults = flp_mults_per_report(s, kind)
+        per_mul = OPS_PER_F128_MUL if s.field_size == 16 else OPS_PER_F64_MUL
+        achieved = mults * per_mul * nlaunch / avg_launch_s / 1e12
+        roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": round(VALU_PEAK_TOPS, 1),
+                "unit": "Tops/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                "kernel": dname, "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                "model": (f"{mults} {'F128' if s.field_size == 16 else 'F64'} mults/report "
+                          f"(prio-style FLP query, SURVEY §8(d)) x {per_mul} int32 ops x {nlaunch} "
+                          f"reports/launch")}
     else:
         roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": None, "traffic": None, "kernel": dname,
@@ -870,6 +910,7 @@ def main():
         "data": f"synthetic: {B} distinct reports/GPU (SURVEY §8(d) recipe; shares made by the GPU "
                 f"client shard), resident in HBM",
         "config": {"workload": label, "xof": "XofTurboShake128" if turbo else "XofShake128",
+                   "engine_options": dict(engine_opts), "schedule": f"overlap {args.overlap}",
                    "reports_per_gpu_per_step": B, "job_workers_per_gpu": W,
                    "parallelism": f"report-sharded x{world}, {W} job stream(s)/GPU, "
                                   + ("RCCL all-gather merge" if args.merge == "rccl" else

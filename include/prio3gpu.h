@@ -133,6 +133,20 @@ int prio3gpu_ctx_sync(prio3gpu_ctx* ctx);
  * (Janus runs aggregation jobs concurrently, aggregator/src/binary_utils/job_driver.rs:119-216);
  * order work across contexts with prio3gpu_ctx_wait and finish with prio3gpu_ctx_sync. */
 int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
+/* Engine options of a context (all default to the measured-fastest path; each alternative is
+ * parity-tested against the oracle; value 0/1 for switches):
+ *   "speculate"     1: accumulate from k_jr's per-wave column sums; 0: direct accumulation
+ *   "wires_mfma"    1: SumVec (chunk > 64) wire pass on the matrix cores; 0: VALU k_flp_wires
+ *   "wires_cols"    1: chunk <= 64 lane-per-column wire pass; 0: VALU k_flp_wires
+ *   "sum_split"     1: Sum's FLP query on two waves per 64 reports; 0: one lane per report
+ *   "fused_helper"  1: FixedPoint helper XOF pipeline (k_helper_xof); 0: exact two-pass path
+ *   "jr_ring"       1: FixedPoint leader joint-rand part via k_jr_ring; 0: k_jr
+ *   "spread"        1: latency-bound sponge launches take one CU per workgroup
+ *   "expand_lds", "jr_lds"  dynamic LDS bytes per k_expand / k_jr block (0 = none): caps those
+ *                   kernels' occupancy so another context's kernels fit beside them
+ *   "exact_squeeze" test switch: every XOF squeeze takes the exact per-element rejection path
+ * The engine reads no environment variables.  PRIO3GPU_E_ARG for an unknown name. */
+int prio3gpu_ctx_set_option(prio3gpu_ctx* ctx, const char* name, int64_t value);
 /* Work queued on `ctx` from now on starts only after all work queued on `other` so far. */
 int prio3gpu_ctx_wait(prio3gpu_ctx* ctx, prio3gpu_ctx* other);
 /* The same in two steps: mark what is queued on `ctx` now; later make another context wait for

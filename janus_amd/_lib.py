@@ -102,6 +102,7 @@ def _declare(lib):
                                            c.c_char_p, c.c_int, c.c_int, c.POINTER(P)]),
         "prio3gpu_ctx_destroy": (c.c_int, [P]),
         "prio3gpu_ctx_set_async": (c.c_int, [P, c.c_int]),
+        "prio3gpu_ctx_set_option": (c.c_int, [P, c.c_char_p, c.c_int64]),
         "prio3gpu_ctx_wait": (c.c_int, [P, P]),
         "prio3gpu_ctx_mark": (c.c_int, [P, c.POINTER(c.c_int)]),
         "prio3gpu_ctx_wait_mark": (c.c_int, [P, P, c.c_int]),
@@ -187,7 +188,8 @@ def _declare(lib):
 # Every symbol include/prio3gpu.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "prio3gpu_ctx_create", "prio3gpu_ctx_create2", "prio3gpu_ctx_destroy", "prio3gpu_ctx_sizes",
-    "prio3gpu_ctx_sync", "prio3gpu_ctx_set_async", "prio3gpu_ctx_wait", "prio3gpu_ctx_mark",
+    "prio3gpu_ctx_sync", "prio3gpu_ctx_set_async", "prio3gpu_ctx_set_option", "prio3gpu_ctx_wait",
+    "prio3gpu_ctx_mark",
     "prio3gpu_ctx_wait_mark",
     "prio3gpu_prepare_init_xof", "prio3gpu_prepare_init_query",
     "prio3gpu_ctx_stream", "prio3gpu_state_create", "prio3gpu_state_destroy",

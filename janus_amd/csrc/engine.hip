@@ -17,7 +17,6 @@
 #include "errors.h"
 #include "prio3_kernels.h"
 #include "fpvec_kernels.h"
-#include "helper_sponge.h"
 #include "wires_mfma.h"
 
 using namespace p3g;
@@ -143,20 +142,20 @@ struct DevBuf {
 // One id per kernel, named exactly as rocprofv3 reports it (kernel-trace names are the
 // template-stripped function names), so the bench's HIP-event table and the profiles agree.
 enum KernelId {
-  KID_QUERY = 0, KID_EXPAND, KID_HELPER_XOF, KID_JR, KID_FLP_WEIGHTS, KID_FLP_QUERY,
-  KID_FLP_WIRES, KID_FPV_WEIGHTS, KID_FPV_WIRES0, KID_FPV_WIRES1, KID_FPV_FINAL, KID_DECIDE,
-  KID_FPV_DECIDE, KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE,
-  KID_SHARD_SEEDS, KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META,
-  KID_REPORT_META_FOLD, KID_FLP_WEIGHTS_WAVE, KID_SHARD_NORM, KID_JR_RING, KID_FLP_QUERY_LANE,
-  KID_FLP_WIRES_COLS, KID_HELPER_SPONGE, KID_FLP_WIRES_MFMA, KID_COUNT
+  KID_QUERY = 0, KID_EXPAND, KID_HELPER_XOF, KID_JR, KID_FLP_WEIGHTS, KID_FLP_WIRES,
+  KID_FPV_WEIGHTS, KID_FPV_WIRES0, KID_FPV_WIRES1, KID_FPV_FINAL, KID_DECIDE, KID_FPV_DECIDE,
+  KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE, KID_SHARD_SEEDS,
+  KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META, KID_REPORT_META_FOLD,
+  KID_SHARD_NORM, KID_JR_RING, KID_FLP_QUERY_LANE, KID_FLP_WIRES_COLS, KID_FLP_WIRES_MFMA,
+  KID_FLP_QUERY_SUM, KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
-    "k_query_rand", "k_expand", "k_helper_xof", "k_jr", "k_flp_weights", "k_flp_query",
-    "k_flp_wires", "k_fpv_weights", "k_fpv_wires0", "k_fpv_wires1", "k_fpv_finalize", "k_decide",
-    "k_fpv_decide", "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge",
-    "k_out_shares", "k_merge", "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove",
-    "k_shard_proof", "k_report_meta", "k_report_meta_fold", "k_flp_weights_wave", "k_shard_norm",
-    "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols", "k_helper_sponge", "k_flp_wires_mfma"};
+    "k_query_rand", "k_expand", "k_helper_xof", "k_jr", "k_flp_weights", "k_flp_wires",
+    "k_fpv_weights", "k_fpv_wires0", "k_fpv_wires1", "k_fpv_finalize", "k_decide", "k_fpv_decide",
+    "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge", "k_out_shares", "k_merge",
+    "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove", "k_shard_proof", "k_report_meta",
+    "k_report_meta_fold", "k_shard_norm", "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols",
+    "k_flp_wires_mfma", "k_flp_query_sum"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -192,35 +191,19 @@ struct prio3gpu_ctx {
   DevBuf io[6];
   DevBuf perm, chunks, partials, pcounts, spec_idx;
   std::vector<uint32_t> h_perm, h_chunk_begin, h_chunk_slot;
-  bool speculate = true;  // k_jr column sums feed the accumulation (PRIO3GPU_SPECULATE=0 disables)
-  bool fused_helper = true;  // FPVec helper: k_helper_xof (PRIO3GPU_FUSED_HELPER=0 disables)
-  bool fused_helper_all = false;  // A/B: every Field128 type's helper via k_helper_xof (=2)
-  uint32_t hx_depth = 2;          // A/B: ring depth of that variant (PRIO3GPU_HX_DEPTH=4)
-  bool hx_spec = true;            // A/B: k_helper_xof's storer column sums (PRIO3GPU_HX_SPEC=0: off)
-  // Sum/SumVec/Histogram helper: expansion + joint-rand-part sponges in one pass (k_helper_sponge,
-  // PRIO3GPU_HELPER_SPONGE=1).  Off: measured no faster than k_expand + k_jr (SumVec 72.7 vs
-  // 71.7 ms, Histogram 8.2 vs 7.8, Sum 2.88 vs 2.85 ms/step; 188 VGPRs = 2 waves/SIMD,
-  // profiles/r03/sponge_helper_fused_r3i.log, bench_r3j_*.log)
-  bool helper_sponge = false;
-  bool force_fallback = false;    // test switch (PRIO3GPU_TEST_FALLBACK=1): every lane falls back
-  size_t hx_lds = 0;         // tuning: dynamic LDS per k_helper_xof block (PRIO3GPU_HX_LDS)
-  // Latency-bound sponge launches with fewer waves than CUs (FixedPoint: a few thousand reports)
-  // take one CU per workgroup: the dispatcher otherwise packs several workgroups, and the two
-  // contexts' kernels, onto shared SIMDs (config E: helper XOF 2.47 s -> 1.60 s per step).
-  bool spread = true;        // PRIO3GPU_SPREAD=0 disables
-  bool jr_ring = true;       // FixedPoint joint-rand part via k_jr_ring (PRIO3GPU_JR_RING=0: k_jr)
+  // Engine options (prio3gpu_ctx_set_option; include/prio3gpu.h lists them).  The defaults are the
+  // measured-fastest paths; every alternative is parity-tested against the oracle.
+  bool speculate = true;     // "speculate": accumulation from k_jr's column sums (0: direct)
+  bool fused_helper = true;  // "fused_helper": FixedPoint helper via k_helper_xof (0: two-pass)
+  bool spread = true;        // "spread": one CU per workgroup for latency-bound sponge launches
+  bool jr_ring = true;       // "jr_ring": FixedPoint leader joint-rand part via k_jr_ring
+  bool wires_mfma = true;    // "wires_mfma": SumVec chunk > 64 wire pass on the matrix cores
+  bool wires_cols = true;    // "wires_cols": chunk <= 64 lane-per-column wire pass
+  bool sum_split = true;     // "sum_split": Sum's FLP query on two waves per 64 reports
+  size_t expand_lds = 0;     // "expand_lds": dynamic LDS per k_expand block (occupancy cap)
+  size_t jr_lds = 0;         // "jr_lds": dynamic LDS per k_jr block (occupancy cap)
   uint32_t cus = 0;          // compute units of the device
-  bool flp_query_lane = true;    // Count/Sum: k_flp_query_lane; PRIO3GPU_FLPQ_BLOCK=1: k_flp_query
-  bool flp_weights_lane = true;  // k_flp_weights (lane/report); PRIO3GPU_FLPW_WAVE=1: the wave form
-  uint32_t wires_slots = 256;  // k_flp_wires (column, row group) slots per block (tuning knob)
-  bool wires_cols = true;      // chunk <= 64: k_flp_wires_cols; PRIO3GPU_WIRES_COLS=0: k_flp_wires
-  bool wrow_align = false;     // PRIO3GPU_WROW_ALIGN=1: weight rows at a 128-B pitch (A/B)
-  size_t expand_lds = 0;       // PRIO3GPU_EXPAND_LDS: k_expand occupancy cap (A/B)
-  bool wires_mfma = true;      // SumVec chunk > 64: k_flp_wires_mfma; PRIO3GPU_WIRES_MFMA=0: k_flp_wires
-  bool wires_mfma_short = false;  // chunk 8..32 (Histogram): k_flp_wires_mfma<SHORT>; opt-in
-                                  // until measured (PRIO3GPU_WIRES_MFMA_SHORT=1)
   DevBuf fallback;           // k_helper_xof's non-canonical-element counter
-  size_t jr_lds = 0;      // tuning: dynamic LDS per k_jr block (PRIO3GPU_JR_LDS; caps blocks/CU)
   Prof prof;
   // async mode (prio3gpu_ctx_set_async): calls whose buffers are all device memory return once
   // their work is queued; cross-context order via prio3gpu_ctx_wait
@@ -645,7 +628,6 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     st->spec_e1 = se1;
   }
   CRows meas, proof, blinds;
-  const uint32_t* jr_gate = nullptr;
   const size_t in_pitch = input_pitch(st);
   if (st->agg_id == 0) {
     meas = CRows{d_in, in_pitch};
@@ -657,23 +639,20 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     bool fused_done = false;
     if constexpr (FO::ES == 16) {
       // Few huge reports: the two helper sponges (expansion, joint-rand part) in lockstep.
-      if ((g.kind == KIND_FPVEC || c->fused_helper_all) && c->fused_helper && g.jr_len > 0) {
+      if (g.kind == KIND_FPVEC && c->fused_helper && g.jr_len > 0) {
         CHK(c->fallback.ensure(4));
         uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
         HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
         {
           PROF(KID_HELPER_XOF);
-          auto kern = (g.kind == KIND_FPVEC || c->hx_depth == 4) ? k_helper_xof<kHxDepth>
-                                                                   : k_helper_xof<2>;
-          hipLaunchKernelGGL(kern, dim3((N + kHxRows - 1) / kHxRows),
+          hipLaunchKernelGGL(k_helper_xof<kHxDepth>, dim3((N + kHxRows - 1) / kHxRows),
                              dim3(3 * kHxRows),
-                             c->hx_lds ? std::min<size_t>(c->hx_lds, kSpreadLds)
-                                       : (spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0),
+                             spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0,
                              c->stream, g, N,
                              CRows{d_in, in_pitch}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
                              Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb,
-                             c->hx_spec ? spec_lo : nullptr, spec_cy);
+                             spec_lo, spec_cy);
         }
         uint32_t h_fb = 0;
         HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -681,40 +660,23 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
         fused_done = h_fb == 0;  // else: a non-canonical element; redo the exact two-pass path
       }
     }
-    if (fused_done) {  // the storer wave wrote the speculative column sums (unless hx_spec is off)
-      if (!c->hx_spec) st->spec_ok = false;
+    if (fused_done) {  // the storer wave wrote the speculative column sums
       st->meas_rows = CRows{mo.base, mo.stride};
       st->proof_rows = CRows{po.base, po.stride};
       st->n = n;
       st->xof_done = true;
       return 0;
     }
-    const uint32_t* gate = nullptr;  // k_expand / k_jr run only if the fused pass fell back
-    if constexpr (FO::ES == 16) {
-      if (c->helper_sponge && g.jr_len > 0 && g.kind != KIND_FPVEC) {
-        CHK(c->fallback.ensure(4));
-        uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
-        HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
-        PROF(KID_HELPER_SPONGE);
-        hipLaunchKernelGGL(k_helper_sponge, grid1(n, TPB), dim3(TPB), (TPB / 64) * kJrWaveLds,
-                           c->stream, g, N, CRows{d_in, in_pitch}, nonces, pub, mo, po,
-                           Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
-                           Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb, spec_lo, spec_cy,
-                           2u * se0, 2u * se1, c->force_fallback ? 1u : 0u);
-        gate = fb;
-      }
-    }
     {
       PROF(KID_EXPAND);
       // c->expand_lds (PRIO3GPU_EXPAND_LDS, A/B knob): unused dynamic LDS that caps the blocks
       // per CU, i.e. k_expand's occupancy
       hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), c->expand_lds, c->stream, g, N,
-                         (uint32_t)st->agg_id, CRows{d_in, in_pitch}, mo, po, d_status, gate);
+                         (uint32_t)st->agg_id, CRows{d_in, in_pitch}, mo, po, d_status);
     }
     meas = CRows{mo.base, mo.stride};
     proof = CRows{po.base, po.stride};
     blinds = CRows{d_in + 32, in_pitch};
-    jr_gate = gate;
   }
   bool ring_done = false;
   if constexpr (FO::ES == 16) {
@@ -741,7 +703,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
       hipLaunchKernelGGL(k_jr<FO>, grid1(n, tpb), dim3(tpb), jr_lds, c->stream, g, N,
                          (uint32_t)st->agg_id, nonces, pub, blinds, meas, Rows{st->part.u8(), 16},
                          Rows{st->seed.u8(), 16}, Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status,
-                         spec_lo, spec_cy, jr_gate);
+                         spec_lo, spec_cy);
     }
   }
   HIPCHK(hipGetLastError());
@@ -749,6 +711,69 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
   st->proof_rows = proof;
   st->n = n;
   st->xof_done = true;
+  return 0;
+}
+
+// ParallelSum types (SumVec, Histogram, Field128): the FLP query in two kernels -- the Lagrange
+// weights and the rest of the verifier except the wires (k_flp_weights: lane per report,
+// latency-bound), then the wire pass over the measurement share (HBM streaming).
+int launch_psum_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, CRows proof,
+                      uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  const uint32_t es = g.es;
+  const uint32_t N = (uint32_t)n;
+  // weight rows (row-major), then k_flp_weights' element-major scratch (calls x n entries)
+  const WMat wrows{st->w.u8(), (size_t)flp_w_len(g) * es, (size_t)es};
+  uint8_t* wscr = st->w.u8() + (size_t)N * flp_w_len(g) * es;
+  const CRows jr{st->jr.u8(), (size_t)g.jr_len * es};
+  const Rows prep{st->prep.u8(), g.prep_share_len};
+  {
+    PROF(KID_FLP_WEIGHTS);
+    hipLaunchKernelGGL(k_flp_weights, grid1(n, kFwThreads), dim3(kFwThreads), 0, c->stream, g, N,
+                       proof, CRows{st->t.u8(), 16}, jr, CRows{st->part.u8(), 16}, prep, d_status,
+                       wrows, wscr);
+  }
+  if (g.chunk <= 64 && c->wires_cols) {
+    // G = next_pow2(chunk) lanes per report, lane = column (Histogram, small SumVec/CountVec)
+    uint32_t lg = 0;
+    while ((1u << lg) < g.chunk) ++lg;
+    PROF(KID_FLP_WIRES_COLS);
+    hipLaunchKernelGGL(k_flp_wires_cols, grid1((size_t)N << lg, 256), dim3(256), 0, c->stream, g, N,
+                       lg, meas, wrows, jr, prep, d_status);
+  } else if (c->wires_mfma && g.kind == KIND_SUMVEC && g.chunk > 64 && g.calls <= kWmMaxCalls &&
+             wires_mfma_e_bytes(g.calls) + 16 <= 64 * 1024) {
+    // byte-limb convolution on v_mfma_i32_32x32x32_i8 (wires_mfma.h): a wave per 32 columns
+    const uint32_t nwv = std::min(4u, (g.chunk + 31) / 32);
+    PROF(KID_FLP_WIRES_MFMA);
+    hipLaunchKernelGGL(k_flp_wires_mfma, dim3(N), dim3(64 * nwv), wires_mfma_e_bytes(g.calls) + 16,
+                       c->stream, g, N, meas, wrows, jr, prep, d_status);
+  } else {
+    // the VALU wire pass: block per report, (column, row group) slots; short reports get >= 4
+    // rows per thread (Histogram256: H 16 -> 4 took 18.0 -> 6.1 ms/step,
+    // profiles/r02/ab_hist_slots*.log)
+    constexpr uint32_t kSlots = 256;
+    FlpDims dims;
+    uint32_t nthr;
+    dims.rp_len = std::max(g.chunk, g.calls) + 1;
+    dims.cols = g.chunk;
+    if (g.chunk <= kSlots) {
+      dims.H = std::min(kSlots / g.chunk, std::max(1u, g.calls / 4));
+      nthr = ((dims.H * g.chunk + 63) / 64) * 64;
+    } else {
+      dims.H = 1;
+      nthr = 256;
+    }
+    size_t lds2 = (size_t)16 * (2 * (size_t)g.calls + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
+    lds2 = (lds2 + 15) & ~(size_t)15;
+    if (lds2 > 160 * 1024) {
+      set_err("FLP wire pass LDS requirement %zu too large", lds2);
+      return PRIO3GPU_E_ARG;
+    }
+    PROF(KID_FLP_WIRES);
+    hipLaunchKernelGGL(k_flp_wires<Field128Ops>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims,
+                       meas, wrows, jr, prep, d_status);
+  }
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
@@ -773,104 +798,30 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
   // FLP query: block per report.  ParallelSum types (SumVec, Histogram) split it in two: the
   // weights (power tables, NTTs, gadget outputs; latency-bound, 2 waves) and the wire pass over
   // the measurement share (HBM streaming, many blocks in flight).
-  FlpDims dims;
-  uint32_t nthr;
-  dims.rp_len = std::max(g.chunk, g.calls) + 1;
   const bool psum = (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM);
-  if (psum) {
-    dims.cols = g.chunk;
-    if (g.chunk <= c->wires_slots) {
-      // row groups: up to the slot budget, but at least ~4 rows per thread, so that short
-      // reports (Histogram256: 16 calls) do not spend a block of mostly idle threads per report
-      // (A/B, profiles/r02/ab_hist_slots*.log: H 16 -> 4 took k_flp_wires 18.0 -> 6.1 ms/step)
-      dims.H = c->wires_slots / g.chunk;
-      dims.H = std::min(dims.H, std::max(1u, g.calls / 4));
-      nthr = ((dims.H * g.chunk + 63) / 64) * 64;
-    } else {
-      dims.H = 1;
-      nthr = 256;
-    }
-  } else {
-    dims.cols = 1;
-    dims.H = 1;
-    nthr = 64;
+  if constexpr (FO::ES == 16) {
+    if (psum) return launch_psum_query(c, st, n, meas, proof, d_status);
   }
-  const size_t esz = sizeof(typename FO::T);
-  FlpDims d1 = dims;
-  uint32_t nthr1 = nthr;
-  if (psum) {
-    d1.H = 0;
-    nthr1 = 128;
-  }
-  size_t lds = esz * (6 * (size_t)g.m + d1.rp_len + 2 * (size_t)d1.H * d1.cols + nthr1 + 128) + 16;
-  lds = (lds + 15) & ~(size_t)15;
-  if (lds > 160 * 1024) {
-    set_err("FLP LDS requirement %zu too large", lds);
+  if (g.kind != KIND_COUNT && g.kind != KIND_SUM) {
+    set_err("no FLP query for VDAF kind %u", g.kind);
     return PRIO3GPU_E_ARG;
   }
-  // weight rows (row-major), then k_flp_weights' element-major scratch (calls x n entries)
-  WMat wrows{nullptr, 0, 0};
-  if (psum) wrows = WMat{st->w.u8(), (size_t)flp_w_pitch(g, c->wrow_align) * es, (size_t)es};
-  uint8_t* wscr = psum ? st->w.u8() + (size_t)N * flp_w_pitch(g, c->wrow_align) * es : nullptr;
-  if (psum && FO::ES == 16 && c->flp_weights_lane) {
-    PROF(KID_FLP_WEIGHTS);
-    hipLaunchKernelGGL(k_flp_weights, grid1(n, kFwThreads), dim3(kFwThreads), 0, c->stream, g, N,
-                       proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
-                       wrows, wscr);
-  } else if (psum && g.m <= 128 && g.chunk <= 128) {
-    PROF(KID_FLP_WEIGHTS_WAVE);
-    hipLaunchKernelGGL(k_flp_weights_wave<FO>, grid1(n, 4), dim3(256), 0, c->stream, g, N, proof,
-                       CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
-                       wrows);
-  } else if ((g.kind == KIND_COUNT || g.kind == KIND_SUM) && c->flp_query_lane) {
+  if constexpr (FO::ES == 16) {
+    if (g.kind == KIND_SUM && c->sum_split && g.arity == 1) {
+      PROF(KID_FLP_QUERY_SUM);
+      hipLaunchKernelGGL(k_flp_query_sum, grid1(n, kFqsReports), dim3(2 * kFqsReports), 0,
+                         c->stream, g, N, meas, proof, CRows{st->t.u8(), 16},
+                         CRows{st->jr.u8(), (size_t)g.jr_len * es}, CRows{st->part.u8(), 16},
+                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
+      HIPCHK(hipGetLastError());
+      return 0;
+    }
+  }
+  {
     PROF(KID_FLP_QUERY_LANE);
     hipLaunchKernelGGL(k_flp_query_lane<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, meas,
                        proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                        CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status);
-  } else {
-    PROF(KID_FLP_QUERY);
-    hipLaunchKernelGGL(k_flp_query<FO>, dim3(N), dim3(nthr1), lds, c->stream, g, N, d1, meas, proof,
-                       CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
-                       wrows);
-  }
-  if (psum) {
-    size_t lds2 = esz * (2 * (size_t)g.calls + 2 * (size_t)dims.H * dims.cols + nthr) + 16;
-    lds2 = (lds2 + 15) & ~(size_t)15;
-    const bool mfma_ok = FO::ES == 16 && c->wires_mfma && c->flp_weights_lane &&
-                         g.calls <= kWmMaxCalls;
-    if (mfma_ok && c->wires_mfma_short && g.chunk >= 8 && g.chunk <= 32 &&
-        4 * wires_mfma_e_bytes(g.calls) <= 64 * 1024) {
-      // short rows (Histogram): a wave per report on v_mfma_i32_32x32x32_i8 (wires_mfma.h)
-      PROF(KID_FLP_WIRES_MFMA);
-      hipLaunchKernelGGL(k_flp_wires_mfma<true>, grid1(N, 4), dim3(256),
-                         4 * wires_mfma_e_bytes(g.calls), c->stream, g, N, meas, wrows,
-                         CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
-    } else if (FO::ES == 16 && g.chunk <= 64 && c->wires_cols) {
-      uint32_t lg = 0;
-      while ((1u << lg) < g.chunk) ++lg;
-      PROF(KID_FLP_WIRES_COLS);
-      hipLaunchKernelGGL(k_flp_wires_cols, grid1((size_t)N << lg, 256), dim3(256), 0, c->stream, g,
-                         N, lg, meas, wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
-    } else if (mfma_ok && g.kind == KIND_SUMVEC && g.chunk > 64 &&
-               wires_mfma_e_bytes(g.calls) + 16 <= 64 * 1024) {
-      // byte-limb convolution on v_mfma_i32_32x32x32_i8 (wires_mfma.h): a wave per 32 columns
-      const uint32_t nwv = std::min(4u, (g.chunk + 31) / 32);
-      PROF(KID_FLP_WIRES_MFMA);
-      hipLaunchKernelGGL(k_flp_wires_mfma<false>, dim3(N), dim3(64 * nwv),
-                         wires_mfma_e_bytes(g.calls) + 16, c->stream, g, N, meas, wrows,
-                         CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
-    } else {
-      PROF(KID_FLP_WIRES);
-      hipLaunchKernelGGL(k_flp_wires<FO>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims, meas,
-                         wrows, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
-    }
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -1172,44 +1123,11 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
   *out = nullptr;
   HIPCHK(hipSetDevice(device));
   auto* c = new prio3gpu_ctx();
-  if (const char* sp = getenv("PRIO3GPU_SPECULATE")) c->speculate = sp[0] != '0';
-  if (const char* fh = getenv("PRIO3GPU_FUSED_HELPER")) {
-    c->fused_helper = fh[0] != '0';
-    c->fused_helper_all = fh[0] == '2';
-  }
-  if (const char* fq = getenv("PRIO3GPU_FLPQ_BLOCK")) c->flp_query_lane = fq[0] == '0';
-  if (const char* wc = getenv("PRIO3GPU_WIRES_COLS")) c->wires_cols = wc[0] != '0';
-  if (const char* wm = getenv("PRIO3GPU_WIRES_MFMA")) c->wires_mfma = wm[0] != '0';
-  if (const char* wa = getenv("PRIO3GPU_WROW_ALIGN")) c->wrow_align = wa[0] == '1';
-  if (const char* el = getenv("PRIO3GPU_EXPAND_LDS"))
-    c->expand_lds = std::min<size_t>(strtoull(el, nullptr, 10), 64 * 1024);
-  if (const char* ws = getenv("PRIO3GPU_WIRES_MFMA_SHORT")) c->wires_mfma_short = ws[0] == '1';
-  if (const char* fw = getenv("PRIO3GPU_FLPW_WAVE")) c->flp_weights_lane = fw[0] == '0';
-  if (const char* ws = getenv("PRIO3GPU_WIRES_SLOTS")) {
-    const long v = strtol(ws, nullptr, 10);
-    if (v >= 64 && v <= 1024) c->wires_slots = (uint32_t)v;
-  }
-  if (const char* jl = getenv("PRIO3GPU_JR_LDS")) c->jr_lds = strtoull(jl, nullptr, 10);
-  if (const char* hl = getenv("PRIO3GPU_HX_LDS")) c->hx_lds = strtoull(hl, nullptr, 10);
-  if (const char* sp = getenv("PRIO3GPU_SPREAD")) c->spread = sp[0] != '0';
-  if (const char* jg = getenv("PRIO3GPU_JR_RING")) c->jr_ring = jg[0] != '0';
-  if (const char* hs = getenv("PRIO3GPU_HX_SPEC")) c->hx_spec = hs[0] != '0';
-  if (const char* hd = getenv("PRIO3GPU_HX_DEPTH")) c->hx_depth = hd[0] == '4' ? 4u : 2u;
-  if (const char* hp = getenv("PRIO3GPU_HELPER_SPONGE")) c->helper_sponge = hp[0] == '1';
-  if (const char* tf = getenv("PRIO3GPU_TEST_FALLBACK")) c->force_fallback = tf[0] == '1';
   {
     int cu = 0;
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
       cu = 0;  // unknown: no spreading
     c->cus = (uint32_t)cu;
-  }
-  // Test switch: every XOF squeeze takes the exact per-element rejection path (the fast path's
-  // bulk stores are skipped), and the FixedPoint helper runs its exact two-pass XOF.
-  const char* ex = getenv("PRIO3GPU_EXACT_SQUEEZE");
-  const bool exact_squeeze = ex && ex[0] == '1';
-  if (exact_squeeze) {
-    c->fused_helper = false;
-    c->helper_sponge = false;
   }
   c->device = device;
   memcpy(c->vk, verify_key, 16);
@@ -1224,7 +1142,6 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
     prio3gpu_ctx_destroy(c);
     return rc;
   }
-  c->cfg.exact_squeeze = exact_squeeze ? 1u : 0u;
   c->cfg.xof = xof == PRIO3GPU_XOF_TURBOSHAKE128 ? kXofTurboShake128 : kXofShake128;
   *out = c;
   return 0;
@@ -1292,7 +1209,7 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   rc |= st->msg.ensure(N * 16);
   rc |= st->status.ensure(N);
   if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM)
-    rc |= st->w.ensure(N * (size_t)(flp_w_pitch(g, true) + g.calls) * g.es);  // rows + scratch
+    rc |= st->w.ensure(N * (size_t)(flp_w_len(g) + g.calls) * g.es);  // rows + scratch
   if (g.kind == KIND_FPVEC) {
     rc |= st->w.ensure(N * (size_t)fpv_w_layout(g).len * 16);
     rc |= st->fpart.ensure(N * (size_t)fpv_rows(g) * g.chunk * 32);
@@ -1608,6 +1525,46 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* c, int on) {
   return 0;
 }
 
+int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
+  if (!c || !name) {
+    set_err("null argument");
+    return PRIO3GPU_E_ARG;
+  }
+  const std::string k(name);
+  const bool on = value != 0;
+  if (k == "speculate") {
+    c->speculate = on;
+  } else if (k == "fused_helper") {
+    c->fused_helper = on;
+  } else if (k == "spread") {
+    c->spread = on;
+  } else if (k == "jr_ring") {
+    c->jr_ring = on;
+  } else if (k == "wires_mfma") {
+    c->wires_mfma = on;
+  } else if (k == "wires_cols") {
+    c->wires_cols = on;
+  } else if (k == "sum_split") {
+    c->sum_split = on;
+  } else if (k == "expand_lds" || k == "jr_lds") {
+    if (value < 0 || value > 160 * 1024) {
+      set_err("option %s: %lld bytes is outside [0, 163840]", name, (long long)value);
+      return PRIO3GPU_E_ARG;
+    }
+    (k == "expand_lds" ? c->expand_lds : c->jr_lds) = (size_t)value;
+  } else if (k == "exact_squeeze") {
+    // every XOF squeeze takes the exact per-element rejection path (test switch); the FixedPoint
+    // helper then runs its exact two-pass XOF
+    c->cfg.exact_squeeze = on ? 1u : 0u;
+    if (on) c->fused_helper = false;
+  } else {
+    set_err("unknown engine option \"%s\"", name);
+    return PRIO3GPU_E_ARG;
+  }
+  c->plan_valid = false;
+  return 0;
+}
+
 int prio3gpu_ctx_mark(prio3gpu_ctx* c, int* out_mark) {
   if (!c || !out_mark) {
     set_err("null argument");
@@ -1844,8 +1801,7 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
   {
     PROF(KID_EXPAND);
     hipLaunchKernelGGL(k_expand<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, 1u,
-                       CRows{d_helper, g.helper_share_len}, hm, hp, (const uint8_t*)nullptr,
-                       (const uint32_t*)nullptr);
+                       CRows{d_helper, g.helper_share_len}, hm, hp, (const uint8_t*)nullptr);
   }
   uint64_t* d_norms = nullptr;  // FixedPointBoundedL2VecSum: squared norm per measurement
   if (g.kind == KIND_FPVEC) {

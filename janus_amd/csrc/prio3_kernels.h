@@ -11,8 +11,11 @@
 //   k_expand       lane/report  helper: XOF(seed, dst1|dst2, [1]) -> meas/proof share (MEAS/10.5 perms)
 //   k_jr           lane/report  joint-rand part over the encoded meas share, corrected seed,
 //                               joint randomness                                      (MEAS/10.5 perms)
-//   k_flp_query    block/report FLP query: circuit output, wire polys at t (Lagrange weights from
-//                               one size-m NTT, no inversions), gadget poly at alpha^k (NTT) and t
+//   k_flp_query_lane  lane/report  FLP query of Count / Sum in registers
+//   k_flp_weights  lane/report  ParallelSum types: Lagrange weights at t (one batched inversion),
+//                               gadget poly at t, circuit output; k_flp_wires_cols /
+//                               k_flp_wires_mfma (wires_mfma.h) / k_flp_wires then stream the
+//                               measurement share once for the wire values
 //   k_decide       lane/report  sum verifier shares, decide, prep msg (1 perm)
 //   k_prepare_next lane/report  prep msg == corrected seed
 //   k_accum_*      segmented modular sum of truncated output shares into per-batch aggregates
@@ -378,16 +381,12 @@ __global__ void __launch_bounds__(256) k_query_rand(Cfg cfg, uint32_t n, uint64_
 // Helper share expansion: meas share XOF(k_meas, dst1, [agg_id]) and proof share
 // XOF(k_proof, dst2, [agg_id]) (prio prepare_init, Share::Helper arms).
 template <class FO>
-// `gate` (optional): run only if *gate != 0 -- the exact path behind k_helper_sponge, which sets
-// it when a lane met a non-canonical element.
 #ifndef P3G_EXPAND_WAVES  // min waves per SIMD for k_expand (A/B knob; 0 = compiler's choice)
 #define P3G_EXPAND_WAVES 0
 #endif
 __global__ void __launch_bounds__(256, P3G_EXPAND_WAVES) k_expand(Cfg cfg, uint32_t n, uint32_t agg_id,
                                                 CRows helper_shares, Rows out_meas,
-                                                Rows out_proof, const uint8_t* status,
-                                                const uint32_t* gate) {
-  if (gate && *gate == 0u) return;
+                                                Rows out_proof, const uint8_t* status) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   if (status && status[r] != ST_OK) return;
@@ -436,9 +435,8 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
                                             CRows public_shares, CRows blinds, CRows meas,
                                             Rows out_part, Rows out_seed, Rows out_jr,
                                             const uint8_t* status, uint64_t* spec_lo,
-                                            uint8_t* spec_cy, const uint32_t* gate) {
+                                            uint8_t* spec_cy) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  if (gate && *gate == 0u) return;  // k_helper_sponge did the work (see k_expand)
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave in block (uniform)
   const uint32_t r0w = blockIdx.x * blockDim.x + 64u * wv;       // first report of this wave
@@ -783,255 +781,11 @@ struct FlpDims {
   uint32_t rp_len;  // entries of the r-power table RP
 };
 
-// W row written by k_flp_query in split mode (ParallelSum types) and read by k_flp_wires:
+// W row written by k_flp_weights (ParallelSum types) and read by the wire passes:
 //   MM[1..calls] | LM[1..calls] | RP[1..c] | B0[c] = L0 s_2j | B1[c] = L0 s_2j+1 - (1/2) sum L_k | gsum
 // (k_flp_weights also appends SMM = sum_k MM[k] and SLM = sum_k LM[k] mod p: k_flp_wires_mfma's
 // offset correction, wires_mfma.h)
 __host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + 3 * cfg.chunk + 3; }
-// row pitch in elements: packed, or rounded up to 128 B (8 Field128 / 16 Field64 elements)
-__host__ __device__ inline uint32_t flp_w_pitch(const Cfg& cfg, bool align128) {
-  const uint32_t q = 128u / cfg.es;
-  return align128 ? (flp_w_len(cfg) + q - 1) / q * q : flp_w_len(cfg);
-}
-
-template <class FO>
-__global__ void __launch_bounds__(256) k_flp_query(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
-                                                   CRows proof, CRows tq, CRows jr, CRows part,
-                                                   Rows out_prep, uint8_t* status, WMat wm) {
-  using T = typename FO::T;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t r = blockIdx.x;
-  if (r >= n) return;
-  if (status[r] != ST_OK) return;
-  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
-  const uint32_t m = cfg.m, logm = cfg.logm, c = dims.cols, H = dims.H;
-  T* TP = reinterpret_cast<T*>(smem);
-  T* NA = TP + 2 * m;
-  T* NB = NA + m;
-  T* LM = NB + m;
-  T* MM = LM + m;
-  T* RP = MM + m;
-  T* PA = RP + dims.rp_len;
-  T* PB = PA + H * c;
-  T* RED = PB + H * c;
-  T* PW = RED + nthr;  // 128-entry scratch for the power tables
-  uint32_t* flag = reinterpret_cast<uint32_t*>(PW + 128);
-  if (tid == 0) *flag = 0u;
-
-  const uint8_t* xr = meas.at(r);
-  const uint8_t* pr = proof.at(r);
-  const uint32_t arity = cfg.arity;
-  const uint32_t gp_len = cfg.gp_len;
-
-  // ---- power tables (Montgomery), one wave each, concurrently:  TP[i] = t^i (i < 2m);
-  //      RP[i] = r^i (i <= c, or <= calls for Sum);  MM[k] = (r^c)^(k-1) (k = 1..calls) ----
-  const T tm = FO::to_mont(FO::load(tq.at(r)));
-  T rm = FO::one_mont();
-  if (cfg.jr_len > 0) rm = FO::to_mont(FO::load(jr.at(r)));
-  {
-    const uint32_t wave = tid >> 6, lane = tid & 63, nw = nthr >> 6;
-    const bool psum = (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM);
-    if (wave == 0) wave_pow_table<FO>(TP, tm, 2 * m, lane);
-    if (wave == (nw > 1 ? 1u : 0u)) {
-      if (psum) wave_pow_table<FO>(RP, rm, c + 1, lane);
-      else if (cfg.kind == KIND_SUM) wave_pow_table<FO>(RP, rm, cfg.calls + 1, lane);
-    }
-    if (psum && wave == (nw > 2 ? 2u : 0u)) {
-      const T rc = mont_pow<FO>(rm, c);  // r^c (each lane, in parallel)
-      wave_pow_table<FO>(MM + 1, rc, cfg.calls, lane);
-    }
-  }
-  __syncthreads();
-  // ---- NTT inputs: NA <- t^(m-1-i) (bit-reversed), NB <- folded gadget poly (bit-reversed) ----
-  bool bad = false;
-  for (uint32_t i = tid; i < m; i += nthr) {
-    const uint32_t bi = bitrev(i, logm);
-    NA[bi] = TP[m - 1 - i];
-    T e = FO::load(pr + (size_t)(arity + i) * FO::ES);
-    bad |= !FO::is_canonical(e);
-    if (i + m < gp_len) {
-      const T e2 = FO::load(pr + (size_t)(arity + i + m) * FO::ES);
-      bad |= !FO::is_canonical(e2);
-      e = FO::add(e, e2);
-    }
-    NB[bi] = e;
-  }
-  if (tid == 0 && FO::eq(TP[m], FO::one_mont())) atomicOr(flag, 2u);  // t^m == 1
-  __syncthreads();
-  ntt2_lds<FO>(cfg, NA, NB, tid, nthr);
-  // ---- Lagrange weights (Montgomery): LM[k] = Y_k * alpha^k / m ; MM[k] = LM[k] * r^(c(k-1)) ----
-  const T inv_m = ld_tw<FO>(cfg, m);  // table entry m holds 1/m (Montgomery)
-  for (uint32_t k = tid; k < m; k += nthr) {
-    T y = FO::mul(NA[k], ld_tw<FO>(cfg, k));
-    y = FO::mul(y, inv_m);
-    LM[k] = y;
-  }
-  __syncthreads();
-  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
-    for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) MM[k] = FO::mul(LM[k], MM[k]);
-  }
-  __syncthreads();
-
-  // ---- p(t) = sum_d c_d t^d (canonical), and the circuit's gadget-output combination ----
-  T pt = FO::zero();
-  for (uint32_t d = tid; d < gp_len; d += nthr) {
-    pt = FO::add(pt, FO::mul(TP[d], FO::load(pr + (size_t)(arity + d) * FO::ES)));
-  }
-  T gsum = FO::zero();  // SumVec/Hist: sum_k p(alpha^k) ; Sum: sum_k r^k p(alpha^k) ; Count: p(alpha)
-  T lsum = FO::zero();  // sum_{k=1..calls} L_k (Montgomery)
-  for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) {
-    if (cfg.kind == KIND_SUM) gsum = FO::add(gsum, FO::mul(RP[k], NB[k]));
-    else gsum = FO::add(gsum, NB[k]);
-    lsum = FO::add(lsum, LM[k]);
-  }
-  block_sum3<FO>(pt, gsum, lsum, RED, tid, nthr);
-
-  // ---- main loop: wire accumulations over the measurement share ----
-  T xsum = FO::zero();  // Histogram sum check
-  uint8_t* outp = out_prep.at(r);
-  const size_t ES = FO::ES;
-  if ((cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) && wm.base != nullptr) {
-    // split mode: hand the weights to k_flp_wires (which streams the measurement share)
-    const uint32_t C = cfg.calls;
-    for (uint32_t k = tid; k < C; k += nthr) {
-      FO::store(wm.el(r, k), MM[k + 1]);
-      FO::store(wm.el(r, C + k), LM[k + 1]);
-    }
-    const T l0 = LM[0];
-    const T half_l = FO::mul(lsum, FO::half());
-    for (uint32_t j = tid; j < c; j += nthr) {
-      const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
-      const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
-      bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
-      FO::store(wm.el(r, 2 * C + j), RP[j + 1]);  // Montgomery
-      FO::store(wm.el(r, 2 * C + c + j), FO::mul(l0, s0));
-      FO::store(wm.el(r, 2 * C + 2 * c + j), FO::sub(FO::mul(l0, s1), half_l));
-    }
-    if (bad) atomicOr(flag, 1u);
-    __syncthreads();
-    if (tid == 0) {
-      FO::store(wm.el(r, 2 * C + 3 * c), gsum);
-      if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
-      FO::store(outp + (size_t)(1 + arity) * ES, pt);
-      const uint8_t* pp = part.at(r);
-      uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
-      st64(dst, ld64(pp));
-      st64(dst + 8, ld64(pp + 8));
-      const uint32_t f = *flag;
-      if (f & 1u) status[r] = ST_INVALID_MESSAGE;
-      else if (f & 2u) status[r] = ST_VDAF_PREP_ERROR;
-    }
-    return;
-  }
-  if (cfg.kind == KIND_SUMVEC || cfg.kind == KIND_HISTOGRAM) {
-    for (uint32_t slot = tid; slot < H * c; slot += nthr) {
-      const uint32_t j = slot % c, h = slot / c;
-      T accA, accB;
-      if constexpr (FO::ES == 16) {
-        // lazy reduction: raw 256-bit products summed, one Montgomery reduction per wire
-        Wide wa, wb;
-        wide_zero(wa);
-        wide_zero(wb);
-        for (uint32_t k = 1 + h; k <= cfg.calls; k += H) {
-          const uint32_t idx = (k - 1) * c + j;
-          if (idx < cfg.meas_len) {
-            const T x = FO::load(xr + (size_t)idx * ES);
-            bad |= !FO::is_canonical(x);
-            wide_mac(wa, MM[k], x);
-            wide_mac(wb, LM[k], x);
-            if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x);
-          }
-        }
-        accA = wide_reduce(wa);
-        accB = wide_reduce(wb);
-      } else {
-        accA = FO::zero();
-        accB = FO::zero();
-        for (uint32_t k = 1 + h; k <= cfg.calls; k += H) {
-          const uint32_t idx = (k - 1) * c + j;
-          if (idx < cfg.meas_len) {
-            const T x = FO::load(xr + (size_t)idx * ES);
-            bad |= !FO::is_canonical(x);
-            accA = FO::add(accA, FO::mul(MM[k], x));
-            accB = FO::add(accB, FO::mul(LM[k], x));
-            xsum = FO::add(xsum, x);
-          }
-        }
-      }
-      PA[h * c + j] = accA;
-      PB[h * c + j] = accB;
-    }
-    __syncthreads();
-    const T l0 = LM[0];
-    const T half_l = FO::mul(lsum, FO::half());  // (1/2) sum_k L_k, canonical
-    for (uint32_t j = tid; j < c; j += nthr) {
-      T a = FO::zero(), b = FO::zero();
-      for (uint32_t h = 0; h < H; ++h) {
-        a = FO::add(a, PA[h * c + j]);
-        b = FO::add(b, PB[h * c + j]);
-      }
-      const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
-      const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
-      bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
-      const T w0 = FO::add(FO::mul(l0, s0), FO::mul(RP[j + 1], a));
-      const T w1 = FO::sub(FO::add(FO::mul(l0, s1), b), half_l);
-      FO::store(outp + (size_t)(1 + 2 * j) * ES, w0);
-      FO::store(outp + (size_t)(2 + 2 * j) * ES, w1);
-    }
-  } else if (cfg.kind == KIND_SUM) {
-    T acc = FO::zero();
-    for (uint32_t k = 1 + tid; k <= cfg.calls; k += nthr) {
-      const T x = FO::load(xr + (size_t)(k - 1) * ES);
-      bad |= !FO::is_canonical(x);
-      acc = FO::add(acc, FO::mul(LM[k], x));
-    }
-    acc = block_sum<FO>(acc, RED, tid, nthr);
-    if (tid == 0) {
-      const T s0 = FO::load(pr);
-      bad |= !FO::is_canonical(s0);
-      FO::store(outp + 1 * ES, FO::add(FO::mul(LM[0], s0), acc));
-    }
-  } else {  // KIND_COUNT: wires f_{0,1} = f_{1,1} = x0
-    if (tid == 0) {
-      const T x = FO::load(xr);
-      bad |= !FO::is_canonical(x);
-      xsum = x;
-      const T lx = FO::mul(LM[1], x);
-      for (uint32_t w = 0; w < 2; ++w) {
-        const T s = FO::load(pr + (size_t)w * ES);
-        bad |= !FO::is_canonical(s);
-        FO::store(outp + (size_t)(1 + w) * ES, FO::add(FO::mul(LM[0], s), lx));
-      }
-    }
-  }
-  if (bad) atomicOr(flag, 1u);
-  if (cfg.kind == KIND_HISTOGRAM) xsum = block_sum<FO>(xsum, RED, tid, nthr);
-  __syncthreads();
-  if (tid == 0) {
-    T v;
-    if (cfg.kind == KIND_COUNT) {
-      v = FO::sub(gsum, xsum);
-    } else if (cfg.kind == KIND_HISTOGRAM) {
-      // jr[1] * range + jr[1]^2 * (sum x - 1/2)
-      const T r1m = FO::to_mont(FO::load(jr.at(r) + ES));
-      const T sc = FO::sub(xsum, FO::half());
-      v = FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc));
-    } else {
-      v = gsum;
-    }
-    FO::store(outp, v);
-    FO::store(outp + (size_t)(1 + arity) * ES, pt);
-    if (cfg.jr_len > 0) {
-      const uint8_t* pp = part.at(r);
-      uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
-      st64(dst, ld64(pp));
-      st64(dst + 8, ld64(pp + 8));
-    }
-    const uint32_t f = *flag;
-    if (f & 1u) status[r] = ST_INVALID_MESSAGE;
-    else if (f & 2u) status[r] = ST_VDAF_PREP_ERROR;
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // FLP query for Count (Mul, 1 call) and Sum (PolyEval(x^2 - x), `bits` calls), one LANE per report:
@@ -1286,14 +1040,161 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
 }
 
 // ------------------------------------------------------------------------------------------------
-// FLP query, ParallelSum types, first half, one WAVE per report (m <= 128, chunk <= 128): the same
-// weights as k_flp_query's split mode, computed in registers with cross-lane shuffles instead of
-// LDS tables and block barriers (no LDS at all, so occupancy is set by VGPRs alone):
-//   * powers of t, r and r^c by wave product scans;
-//   * both size-m NTTs (t^(m-1-i) and the folded gadget poly) as register DIF transforms:
-//     position p = 64e + lane, stage distance h = 64 in-lane, h < 64 via shfl_xor; the result at
-//     position p is X[bitrev(p)], which is the k the lane stores under;
-//   * p(t) with lane l summing coefficients d = l + 64q.
+// FLP query for Sum (Field128), the same arithmetic as k_flp_query_lane split over TWO waves per 64
+// reports, so each wave keeps about half the live state (more waves per SIMD hide the Montgomery
+// chains' latency, which bounds the one-lane form at 2 waves/SIMD):
+//   wave 0 ("H"): Horner on p(t) = sum_i (c_i + t^m c_(i+m)) t^i and the wire fraction
+//                 N/D = sum_(k=0..calls) alpha^k x_k / (t - alpha^k) (k = 0: the proof seed);
+//   wave 1 ("V"): the gadget-output fraction  v = sum_(i<m) F_i G(r alpha^i)  (F = the gadget poly
+//                 folded mod x^m - 1, G(y) = y (y^calls - 1)/(y - 1)), whose numerator and
+//                 denominator it hands to wave 0 through LDS;
+// wave 0 then inverts both denominators with one inversion and writes the prep share.  Products
+// issue as hazard-free triples (mont_mul3).  Bit-identical to k_flp_query_lane (same field values).
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kFqsReports = 64;
+
+__global__ void __launch_bounds__(2 * kFqsReports) k_flp_query_sum(Cfg cfg, uint32_t n, CRows meas,
+                                                                   CRows proof, CRows tq, CRows jr,
+                                                                   CRows part, Rows out_prep,
+                                                                   uint8_t* status) {
+  using FO = Field128Ops;
+  using T = F128;
+  __shared__ __attribute__((aligned(16))) T xch[3][kFqsReports];  // V -> H: vn, vd, extra
+  const uint32_t lane = threadIdx.x & 63u, role = threadIdx.x >> 6;  // role wave-uniform
+  const uint32_t r = blockIdx.x * kFqsReports + lane;
+  const bool live = r < n && status[r] == ST_OK;
+  const uint32_t rr = r < n ? r : n - 1u;  // dead lanes compute on a valid row, store nothing
+  const uint32_t m = cfg.m, calls = cfg.calls, gp_len = cfg.gp_len;
+  const uint8_t* pr = proof.at(rr);
+  const uint8_t* gp = pr + (size_t)cfg.arity * 16;  // gadget poly coefficients (arity 1)
+  const T one = FO::one_mont();
+  const bool half = 2u * calls == m;  // power-of-two bits: y^calls = +-r^calls
+  if (role == 1) {
+    // ---- V: r^m, r^calls, then the fraction over i = m-1 .. 0 ----
+    const T rm = FO::to_mont(FO::load(jr.at(rr)));
+    T rmm = rm, rc = one, b = rm;
+    for (uint32_t q = 0; q < cfg.logm; ++q) {
+      if ((calls >> q) & 1u) rc = FO::mul(rc, b);
+      T idle;
+      mul3<FO>(rmm, rmm, b, b, one, one, rmm, b, idle);
+    }
+    T vn = FO::zero(), vd = one, extra = FO::zero();
+    auto fcoef = [&](uint32_t i) {
+      const T ci = FO::load(gp + (size_t)i * 16);
+      return i + m < gp_len ? FO::add(ci, FO::load(gp + (size_t)(i + m) * 16)) : ci;
+    };
+    if (!FO::eq(rmm, one)) {
+      const T ycm_even = FO::sub(rc, one), ycm_odd = FO::sub(FO::sub(FO::zero(), rc), one);
+      T y = FO::mul(rm, ld_tw<FO>(cfg, m - 1u));
+      T um1 = FO::zero();  // u - 1 for the current i (non-half)
+      if (!half)
+        um1 = FO::sub(FO::mul(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)(m - 1u) * calls) % m))), one);
+      for (uint32_t i = m - 1;; --i) {
+        const T f = fcoef(i);
+        const T e = FO::sub(y, one);
+        const T gm = half ? ((i & 1u) ? ycm_odd : ycm_even) : um1;
+        const uint32_t in = i ? i - 1u : 0u;
+        T yf, g, yn, yfg, vde, vne;
+        mul3<FO>(y, f, gm, vd, rm, ld_tw<FO>(cfg, in), yf, g, yn);
+        if (!half) {  // next iteration's u - 1 (an idle pair: only configs with bits != 2^k)
+          T un, i1, i2;
+          mul3<FO>(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)in * calls) % m)), one, one, one, one,
+                   un, i1, i2);
+          um1 = FO::sub(un, one);
+        }
+        mul3<FO>(yf, g, vd, e, vn, e, yfg, vde, vne);
+        vn = FO::add(vne, yfg);
+        vd = vde;
+        y = yn;
+        if (i == 0) break;
+      }
+    } else {  // r^m == 1 (probability ~m / p): some y_i == 1, where G = calls
+      const T calls_m = FO::to_mont(FO::from_u32(calls));
+      for (uint32_t i = m; i-- > 0;) {
+        const T f = fcoef(i);
+        const T y = FO::mul(rm, ld_tw<FO>(cfg, i));
+        if (FO::is_zero(FO::sub(y, one))) {
+          extra = FO::add(extra, FO::mul(calls_m, f));
+        } else {
+          const T e = FO::sub(y, one);
+          const T yc = FO::mul(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)i * calls) % m)));
+          const T bb = FO::mul(FO::mul(y, f), FO::sub(yc, one));
+          vn = FO::add(FO::mul(vn, e), FO::mul(bb, vd));
+          vd = FO::mul(vd, e);
+        }
+      }
+    }
+    xch[0][lane] = vn;
+    xch[1][lane] = vd;
+    xch[2][lane] = extra;
+    __syncthreads();
+    return;
+  }
+  // ---- H: t^m, Horner and the wire fraction over i = m-1 .. 0 ----
+  const uint8_t* xr = meas.at(rr);
+  bool bad = false;
+  const T tm = FO::to_mont(FO::load(tq.at(rr)));
+  T tmm = tm;
+  for (uint32_t i = 0; i < cfg.logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
+  const bool root = FO::eq(tmm, one);
+  const T cm = FO::mul(FO::sub(tmm, one), ld_tw<FO>(cfg, m));  // (t^m - 1)/m, Montgomery
+  const T s0 = FO::load(pr);
+  bad |= !FO::is_canonical(s0);
+  T pt = FO::zero(), nw0 = FO::zero(), dw = one;
+  for (uint32_t i = m - 1;; --i) {
+    const T ci = FO::load(gp + (size_t)i * 16);
+    const T ch = i + m < gp_len ? FO::load(gp + (size_t)(i + m) * 16) : FO::zero();
+    bad |= !FO::is_canonical(ci) || !FO::is_canonical(ch);
+    const T twi = ld_tw<FO>(cfg, i);
+    T q, P, a;
+    if (i >= 1 && i <= calls) {
+      const T x = FO::load(xr + (size_t)(i - 1) * 16);
+      bad |= !FO::is_canonical(x);
+      const T d = FO::sub(tm, twi);
+      mul3<FO>(tmm, ch, tm, pt, twi, x, q, P, a);
+      T dwn, adw, nwd;
+      mul3<FO>(dw, d, a, dw, nw0, d, dwn, adw, nwd);
+      nw0 = FO::add(nwd, adw);
+      dw = dwn;
+    } else {
+      T idle;
+      mul3<FO>(tmm, ch, tm, pt, one, one, q, P, idle);
+    }
+    pt = FO::add(P, FO::add(ci, q));
+    if (i == 0) break;
+  }
+  {  // the k = 0 wire term: a = the proof seed
+    const T d = FO::sub(tm, one);
+    T nd, sd, dd;
+    mul3<FO>(nw0, d, s0, dw, dw, d, nd, sd, dd);
+    nw0 = FO::add(nd, sd);
+    dw = dd;
+  }
+  __syncthreads();
+  const T vn = xch[0][lane], vd = xch[1][lane], extra = xch[2][lane];
+  // one inversion for both denominators
+  const T inv = inv_mont<FO>(FO::mul(dw, vd));
+  T dinv, vinv, idle;
+  mul3<FO>(inv, vd, inv, dw, one, one, dinv, vinv, idle);
+  T nd, vv;
+  mul3<FO>(nw0, dinv, vn, vinv, one, one, nd, vv, idle);
+  const T w0 = FO::mul(cm, nd);
+  const T v = FO::add(vv, extra);
+  if (!live) return;
+  uint8_t* outp = out_prep.at(r);
+  FO::store(outp, v);
+  FO::store(outp + 16, w0);
+  FO::store(outp + 32, pt);  // (1 + arity) * 16 with arity 1
+  const uint8_t* pp = part.at(r);
+  uint8_t* dst = outp + (size_t)cfg.verifier_len * 16;
+  st64(dst, ld64(pp));
+  st64(dst + 8, ld64(pp + 8));
+  if (bad) status[r] = ST_INVALID_MESSAGE;
+  else if (root) status[r] = ST_VDAF_PREP_ERROR;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Cross-lane helpers for Field elements.
 // ------------------------------------------------------------------------------------------------
 template <class FO>
 DEVI typename FO::T shfl_T(const typename FO::T& v, int src) {
@@ -1323,158 +1224,10 @@ DEVI typename FO::T sel(bool c, const typename FO::T& a, const typename FO::T& b
   return o;
 }
 
-// Occupancy hint for the latency-bound weights kernel (wave-level scans / NTT shuffle chains):
-// more waves per SIMD hide the shuffle + Montgomery latencies.
-#ifndef FLPW_WAVES
-#define FLPW_WAVES __attribute__((amdgpu_waves_per_eu(6)))
-#endif
-template <class FO>
-__global__ void __launch_bounds__(256) FLPW_WAVES k_flp_weights_wave(Cfg cfg, uint32_t n, CRows proof, CRows tq,
-                                                     CRows jr, CRows part, Rows out_prep,
-                                                     uint8_t* status, WMat wm) {
-  using T = typename FO::T;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (r >= n) return;              // wave-uniform
-  if (status[r] != ST_OK) return;  // wave-uniform
-  const uint32_t m = cfg.m, logm = cfg.logm, C = cfg.calls, c = cfg.chunk;
-  const uint32_t arity = cfg.arity, gp_len = cfg.gp_len;
-  const size_t ES = FO::ES;
-  const uint8_t* pr = proof.at(r);
-  const uint8_t* gp = pr + (size_t)arity * ES;
-  const T one = FO::one_mont();
-  bool bad = false;
-
-  // ---- powers of t:  tl = t^lane,  t64 = t^64 ----
-  const T tm = FO::to_mont(FO::load(tq.at(r)));
-  const T ta = wave_pow_scan<FO>(tm, lane);  // t^(lane+1)
-  T tl = shfl_T<FO>(ta, (int)((lane + 63u) & 63u));
-  tl = sel<FO>(lane == 0, one, tl);
-  const T t64 = shfl_T<FO>(ta, 63);
-  const T t128 = FO::mul(t64, t64);
-  const T tmm = shfl_T<FO>(tl, (int)(m & 63u));  // t^m for m < 64
-  const bool tbad = FO::eq(m == 128 ? t128 : (m == 64 ? t64 : tmm), one);
-
-  // ---- gadget poly, coefficients d = lane + 64q (q < 4): p(t), and the sum of the gadget outputs
-  //      sum_{k=1..calls} p(alpha^k) = sum_d c_d S[d mod m] with S[i] = sum_{k=1..calls} alpha^(ik)
-  //      (host table: twiddle entries m+1 .. 2m) -- a dot product instead of a size-m NTT ----
-  T pt = FO::zero(), gsum = FO::zero();
-  {
-    T tp = tl;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t d = lane + 64u * q;
-      if (d < gp_len) {
-        const T cd = FO::load(gp + (size_t)d * ES);
-        bad |= !FO::is_canonical(cd);
-        pt = FO::add(pt, FO::mul(tp, cd));
-        gsum = FO::add(gsum, FO::mul(ld_tw<FO>(cfg, m + 1u + (d & (m - 1u))), cd));
-      }
-      if (q < 3) tp = FO::mul(tp, t64);
-    }
-  }
-  pt = wave_sum<FO>(pt);
-  gsum = wave_sum<FO>(gsum);
-
-  // ---- NTT input (natural order), position p = 64e + lane: t^(m-1-p) ----
-  T A[2];
-  {
-    const T S = shfl_T<FO>(tl, (int)((m - 1u - lane) & 63u));  // t^((m-1-lane) mod 64)
-    if (m == 128) {
-      A[0] = FO::mul(S, t64);  // t^(127-lane)
-      A[1] = S;                // t^(63-lane)
-    } else {
-      A[0] = lane < m ? S : FO::zero();
-      A[1] = FO::zero();
-    }
-  }
-  // ---- DIF NTT: X[k] = sum_i x_i alpha_m^(ik), output at bitrev position ----
-  if (m == 128) {
-    const T w = ld_tw<FO>(cfg, lane);  // alpha_128^lane
-    const T u = A[0], v = A[1];
-    A[0] = FO::add(u, v);
-    A[1] = FO::mul(FO::sub(u, v), w);
-  }
-  const uint32_t E = m == 128 ? 2u : 1u;
-  for (uint32_t h = (m >= 64 ? 32u : m >> 1); h >= 1; h >>= 1) {
-    const T w = ld_tw<FO>(cfg, (lane & (h - 1u)) * (m / (2u * h)));
-    const bool hi = (lane & h) != 0;
-#pragma unroll
-    for (uint32_t e = 0; e < 2; ++e) {
-      if (e < E) {
-        const T oa = shfl_xor_T<FO>(A[e], (int)h);
-        const T sa = hi ? FO::sub(oa, A[e]) : FO::add(A[e], oa);
-        A[e] = hi ? FO::mul(sa, w) : sa;
-      }
-    }
-  }
-  // ---- Lagrange weights LM[k] = Y_k alpha^k / m (alpha^k / m: twiddle entries 2m+1 .. 3m) ----
-  uint32_t K[2];
-  T LMv[2];
-  T lsum = FO::zero();
-#pragma unroll
-  for (uint32_t e = 0; e < 2; ++e) {
-    const uint32_t p = 64u * e + lane;
-    K[e] = bitrev(p & (m - 1u), logm);
-    LMv[e] = FO::mul(A[e], ld_tw<FO>(cfg, 2u * m + 1u + K[e]));
-    if (e < E && p < m && K[e] >= 1u && K[e] <= C) lsum = FO::add(lsum, LMv[e]);
-  }
-  lsum = wave_sum<FO>(lsum);
-  const T l0 = shfl_T<FO>(LMv[0], 0);  // position 0 holds k = 0 (lane 0, e = 0)
-
-  // ---- r powers: RP[j] = r^j,  rc = r^c,  MM[k] = LM[k] rc^(k-1) ----
-  const T rm = FO::to_mont(FO::load(jr.at(r)));
-  const T ra = wave_pow_scan<FO>(rm, lane);  // r^(lane+1)
-  const T r64 = shfl_T<FO>(ra, 63);
-  T rc = shfl_T<FO>(ra, (int)((c - 1u) & 63u));
-  if (c > 64) rc = FO::mul(rc, r64);
-  const T qa = wave_pow_scan<FO>(rc, lane);  // rc^(lane+1)
-  T ql = shfl_T<FO>(qa, (int)((lane + 63u) & 63u));
-  ql = sel<FO>(lane == 0, one, ql);  // rc^lane
-  const T q64 = shfl_T<FO>(qa, 63);
-#pragma unroll
-  for (uint32_t e = 0; e < 2; ++e) {
-    const uint32_t p = 64u * e + lane;
-    const uint32_t k = K[e];
-    const T qk = shfl_T<FO>(ql, (int)((k - 1u) & 63u));  // all lanes shuffle, then select
-    if (e < E && p < m && k >= 1u && k <= C) {
-      T mm = FO::mul(LMv[e], qk);
-      if (k - 1u >= 64u) mm = FO::mul(mm, q64);
-      FO::store(wm.el(r, k - 1u), mm);
-      FO::store(wm.el(r, C + k - 1u), LMv[e]);
-    }
-  }
-  const T half_l = FO::mul(lsum, FO::half());
-#pragma unroll
-  for (uint32_t q = 0; q < 2; ++q) {
-    const uint32_t j = lane + 64u * q;
-    if (j < c) {
-      FO::store(wm.el(r, 2 * C + j), q ? FO::mul(ra, r64) : ra);  // r^(j+1), Montgomery
-      const T s0 = FO::load(pr + (size_t)(2 * j) * ES);
-      const T s1 = FO::load(pr + (size_t)(2 * j + 1) * ES);
-      bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
-      FO::store(wm.el(r, 2 * C + c + j), FO::mul(l0, s0));
-      FO::store(wm.el(r, 2 * C + 2 * c + j), FO::sub(FO::mul(l0, s1), half_l));
-    }
-  }
-  const bool anybad = __any(bad);
-  if (lane == 0) {
-    FO::store(wm.el(r, 2 * C + 3 * c), gsum);
-    uint8_t* outp = out_prep.at(r);
-    if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
-    FO::store(outp + (size_t)(1 + arity) * ES, pt);
-    const uint8_t* pp = part.at(r);
-    uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
-    st64(dst, ld64(pp));
-    st64(dst + 8, ld64(pp + 8));
-    if (anybad) status[r] = ST_INVALID_MESSAGE;
-    else if (tbad) status[r] = ST_VDAF_PREP_ERROR;
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
-// FLP query, ParallelSum types, first half, one LANE per report (Field128).  Same outputs as
-// k_flp_weights_wave, with about half its multiplications and no cross-lane arithmetic:
+// FLP query, ParallelSum types, first half, one LANE per report (Field128).  Same outputs as the
+// round-1 wave-per-report form (since removed), with about half its multiplications and no
+// cross-lane arithmetic:
 //   * Lagrange weights L_k(t) = (alpha^k/m) (t^m - 1) / (t - alpha^k), k = 0..calls, from ONE
 //     batched inversion (Montgomery's trick: prefix products of d_k = t - alpha^k parked in an
 //     element-major scratch, one x^(p-2), a backward pass); t^m - 1 is folded into the inverse,

@@ -52,39 +52,35 @@ typedef int i32x16_t __attribute__((ext_vector_type(16)));
 constexpr uint32_t kWmEDwords = 12;     // 48-byte reversed digit window per (call, wire)
 constexpr uint32_t kWmMaxCalls = 8000;  // |acc| <= calls * 16 * 2^14 < 2^31
 
-
-
-
 DEVI uint64_t shfl_xor_u64(uint64_t v, int m) {
   const uint32_t lo = __shfl_xor((uint32_t)v, m), hi = __shfl_xor((uint32_t)(v >> 32), m);
   return ((uint64_t)hi << 32) | lo;
 }
 
-// SHORT = false: block per report, a wave per 32-column tile (<= 4 waves, then tiles loop).
-// SHORT = true (chunk <= 32: Histogram, short SumVec rows): a wave per report, 4 reports per
-// block, no block barrier; Histogram's v = jr[1] range + jr[1]^2 (sum x - 1/2) needs sum x, which
-// each lane accumulates from the share words it loads anyway.
+
+// Block per report, a wave per 32-column tile (<= 4 waves, then tiles loop).  (A wave-per-report
+// form for short rows, chunk 8..32, measured slower than k_flp_wires_cols -- 3.9 vs 1.66 ms per
+// launch on Histogram256, profiles/r03/ab_wires_mfma_short_r3u.log -- and was removed.)
 __host__ __device__ inline size_t wires_mfma_e_bytes(uint32_t calls) {
   return (size_t)(2 * ((calls + 1) / 2)) * 2 * kWmEDwords * 4;
 }
 
-template <bool SHORT>
 __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRows meas, WMat wm,
                                                          CRows jr, Rows out_prep, uint8_t* status) {
   using FO = Field128Ops;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   if constexpr (P3G_FLP_PRIO > 0) __builtin_amdgcn_s_setprio(P3G_FLP_PRIO);
-  const uint32_t r = SHORT ? blockIdx.x * (blockDim.x >> 6) + wave : blockIdx.x;
-  if (r >= n) return;  // SHORT: wave-uniform, and nothing below waits for other waves
+  const uint32_t r = blockIdx.x;
+  if (r >= n) return;
   if (status[r] != ST_OK) return;
-  const uint32_t nw = SHORT ? 1u : blockDim.x >> 6;  // waves sharing the report
-  const uint32_t wv = SHORT ? 0u : wave;             // this wave's first tile
-  const uint32_t pt = SHORT ? lane : tid, npt = SHORT ? 64u : blockDim.x;  // weight conversion
+  const uint32_t nw = blockDim.x >> 6;  // waves sharing the report
+  const uint32_t wv = wave;             // this wave's first tile
+  const uint32_t pt = tid, npt = blockDim.x;  // weight conversion
   const uint32_t C = cfg.calls, c = cfg.chunk, KQ = (C + 1) / 2;
-  uint32_t* E = reinterpret_cast<uint32_t*>(smem + (SHORT ? wave * wires_mfma_e_bytes(C) : 0));
-  uint32_t* flag = reinterpret_cast<uint32_t*>(smem + wires_mfma_e_bytes(C));  // !SHORT only
-  if (!SHORT && tid == 0) *flag = 0u;
+  uint32_t* E = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* flag = reinterpret_cast<uint32_t*>(smem + wires_mfma_e_bytes(C));
+  if (tid == 0) *flag = 0u;
 
   const uint32_t nn = lane & 31u, h = lane >> 5;
   const uint32_t o = 31u - nn;  // A row s = nn: the fragment is E[o .. o + 15]
@@ -134,17 +130,10 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
       row[2] = make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  if (SHORT) {  // the wave reads only what its own lanes wrote: order the LDS ops, no barrier
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  } else {
-    __syncthreads();
-  }
+  __syncthreads();
 
   // ---- main loop: wave = 32-column tile, K-step q covers calls 2q (h = 0) and 2q + 1 (h = 1) ----
   bool bad = false;
-  uint64_t xs[4] = {0ull, 0ull, 0ull, 0ull};  // SHORT Histogram: this lane's share words, summed
   for (uint32_t tile = wv; tile < NT; tile += nw) {  // 32-column tiles
     const uint32_t j = tile * 32u + nn;
     const bool colok = j < c;
@@ -161,12 +150,6 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
       for (uint32_t u = 0; u < U; ++u) {
         if (q0 + u < KQ) {
           maybe |= __ballot(xv[u].w == 0xFFFFFFFFu);
-          if (SHORT && cfg.kind == KIND_HISTOGRAM) {  // dead slots loaded zero
-            xs[0] += xv[u].x;
-            xs[1] += xv[u].y;
-            xs[2] += xv[u].z;
-            xs[3] += xv[u].w;
-          }
           const i32x4_t b = {(int)(xv[u].x ^ 0x80808080u), (int)(xv[u].y ^ 0x80808080u),
                              (int)(xv[u].z ^ 0x80808080u), (int)(xv[u].w ^ 0x80808080u)};
           const uint32_t* ea = Eh + (size_t)(q0 + u) * 4 * kWmEDwords;
@@ -279,46 +262,9 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
       }
     }
   }
-  if (SHORT) {
-    const uint64_t bm = __ballot(bad);
-    if (cfg.kind == KIND_HISTOGRAM) {
-      // sum x = the wave's word sums (< 2^40 each), reduced mod p as REDC(sum * 2^128)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) xs[i] += shfl_xor_u64(xs[i], m);
-      }
-      if (lane == 0) {
-        uint32_t X[5];
-        uint64_t cr = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint64_t t = xs[i] + cr;
-          X[i] = (uint32_t)t;
-          cr = t >> 32;
-        }
-        X[4] = (uint32_t)cr;
-        Wide wx;  // words 4..8 = sum x
-        wide_zero(wx);
-        wx.lo[4] = X[0];
-        wx.lo[5] = X[1];
-        wx.lo[6] = ((uint64_t)X[3] << 32) | X[2];
-        wx.hi[6] = X[4];
-        const F128 xsum = wide_reduce(wx);
-        const F128 gsum = FO::load(wm.el(r, 2 * C + 3 * c));
-        const F128 r1m = FO::to_mont(FO::load(jr.at(r) + 16));
-        const F128 sc = FO::sub(xsum, FO::half());
-        FO::store(out_prep.at(r), FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc)));
-        if (bm) status[r] = ST_INVALID_MESSAGE;
-      }
-    } else if (lane == 0 && bm) {
-      status[r] = ST_INVALID_MESSAGE;
-    }
-  } else {
-    if (bad) atomicOr(flag, 1u);
-    __syncthreads();
-    if (tid == 0 && (*flag & 1u)) status[r] = ST_INVALID_MESSAGE;
-  }
+  if (bad) atomicOr(flag, 1u);
+  __syncthreads();
+  if (tid == 0 && (*flag & 1u)) status[r] = ST_INVALID_MESSAGE;
 }
 
 }  // namespace p3g

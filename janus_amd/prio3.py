@@ -311,6 +311,13 @@ class Prio3Gpu:
     def sync(self):
         check(lib().prio3gpu_ctx_sync(self._ctx), "sync")
 
+    def set_option(self, name: str, value: int):
+        """Engine option of this context (prio3gpu_ctx_set_option: "speculate", "wires_mfma",
+        "wires_cols", "sum_split", "fused_helper", "jr_ring", "spread", "expand_lds", "jr_lds",
+        "exact_squeeze")."""
+        check(lib().prio3gpu_ctx_set_option(self._ctx, name.encode(), int(value)),
+              f"ctx_set_option({name})")
+
     # -- asynchronous use (include/prio3gpu.h: prio3gpu_ctx_set_async / _wait / _mark) -----------
     def set_async(self, on: bool = True):
         """Calls over device buffers return once queued (host buffers still wait)."""

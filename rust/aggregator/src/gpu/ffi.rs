@@ -145,6 +145,8 @@ extern "C" {
     pub fn prio3gpu_ctx_sizes(ctx: *const prio3gpu_ctx, out: *mut prio3gpu_sizes) -> c_int;
     pub fn prio3gpu_ctx_sync(ctx: *mut prio3gpu_ctx) -> c_int;
     pub fn prio3gpu_ctx_set_async(ctx: *mut prio3gpu_ctx, on: c_int) -> c_int;
+    pub fn prio3gpu_ctx_set_option(ctx: *mut prio3gpu_ctx, name: *const c_char, value: i64)
+                                   -> c_int;
     pub fn prio3gpu_ctx_wait(ctx: *mut prio3gpu_ctx, other: *mut prio3gpu_ctx) -> c_int;
     pub fn prio3gpu_ctx_mark(ctx: *mut prio3gpu_ctx, out_mark: *mut c_int) -> c_int;
     pub fn prio3gpu_ctx_wait_mark(ctx: *mut prio3gpu_ctx, other: *mut prio3gpu_ctx,

@@ -22,3 +22,16 @@ def test_leader_output_shares_match_oracle(name):
     got = leader_output_shares(b.leader_in, KINDS[type(typ).__name__], getattr(typ, "bits", 0),
                                getattr(typ, "length", 0), Sizes, b.vdaf.fld.MODULUS)
     assert np.array_equal(got, b.leader_out)
+
+
+def test_flp_op_model_matches_survey_appendix_b():
+    """bench.py's FLP op model (the roofline of k_flp_query_lane-bound configs) gives
+    Appendix B's per-aggregator multiplication counts: Sum32 ~900, Histogram256 ~4.6K,
+    SumVec(8,1000) ~128K, Count ~14."""
+    import bench
+    from types import SimpleNamespace as NS
+    mk = lambda fs, ml, pl, vl: NS(field_size=fs, meas_len=ml, proof_len=pl, verifier_len=vl)
+    assert bench.flp_mults_per_report(mk(16, 32, 128, 3), 1) == 895
+    assert 4000 <= bench.flp_mults_per_report(mk(16, 256, 95, 34), 3) <= 4700
+    assert 115000 <= bench.flp_mults_per_report(mk(16, 8000, 433, 180), 2) <= 130000
+    assert bench.flp_mults_per_report(mk(8, 1, 5, 4), 0) == 14

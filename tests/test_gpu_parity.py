@@ -368,14 +368,14 @@ def test_fixedpoint16_100k_entries_config_e():
 
 
 @pytest.mark.parametrize("name", ["fp16_3", "fp64_4", "fp16_300"])
-def test_fpvec_helper_two_pass_path_bit_exact(name, monkeypatch):
+def test_fpvec_helper_two_pass_path_bit_exact(name):
     """The FixedPoint helper runs its two sponges fused (k_helper_xof) by default and falls back
     to the exact two-pass k_expand + k_jr when a squeezed element is non-canonical.  The fallback
     cannot be provoked with real seeds (probability ~28/2^64 per element), so force the two-pass
-    path through the context switch and check it too against the oracle's transcript."""
-    monkeypatch.setenv("PRIO3GPU_FUSED_HELPER", "0")
+    path through the context option and check it too against the oracle's transcript."""
     b = batch(name)
     v = gpu_vdaf(b)
+    v.set_option("fused_helper", 0)
     hs = v.new_state(1, b.n)
     hp, hst = v.prepare_init(hs, b.nonces, b.public, b.helper_in)
     assert (hst == 0).all()
@@ -385,18 +385,18 @@ def test_fpvec_helper_two_pass_path_bit_exact(name, monkeypatch):
     np.testing.assert_array_equal(ho, b.helper_out)
 
 
-@pytest.mark.parametrize("env", [{}, {"PRIO3GPU_JR_RING": "0"}, {"PRIO3GPU_SPREAD": "0"}],
+@pytest.mark.parametrize("opts", [{}, {"jr_ring": 0}, {"spread": 0}],
                          ids=["ring", "k_jr_spread", "k_jr_packed"])
 @pytest.mark.parametrize("name", ["fp16_3", "fp16_300"])
-def test_fpvec_leader_jr_variants(name, env, monkeypatch):
+def test_fpvec_leader_jr_variants(name, opts):
     """The leader's FixedPoint joint-rand part runs k_jr_ring (sponge wave + loader wave writing
     the speculative column sums) when few waves fit one per CU, else k_jr.  Every variant gives
     the oracle's prep shares, and its column sums fold into the exact aggregate with a rejected
     row subtracted (report 1's status set before prepare_next; rows past n are clamped copies)."""
-    for k, val in env.items():
-        monkeypatch.setenv(k, val)
     b = batch(name)
     v = gpu_vdaf(b)
+    for k, val in opts.items():
+        v.set_option(k, val)
     ls = v.new_state(0, b.n)
     lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
     assert (lst == 0).all()

@@ -7,8 +7,6 @@ are subtracted again), and tampered reports are rejected after k_jr has already 
 Expected aggregates = plaintext sums of the accepted reports per slot
 (integration_tests/tests/common/mod.rs:225-398 semantics), and both paths agree byte for byte.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -20,16 +18,10 @@ pytestmark = pytest.mark.gpu
 def _vdaf(name, speculate):
     from janus_amd.prio3 import Prio3Gpu
     c = CONFIGS[name]
-    old = os.environ.get("PRIO3GPU_SPECULATE")
-    os.environ["PRIO3GPU_SPECULATE"] = "1" if speculate else "0"
-    try:
-        return Prio3Gpu(c["kind"], bytes(range(16)), bits=c["bits"], length=c["length"],
-                        chunk_length=c["chunk"])
-    finally:
-        if old is None:
-            del os.environ["PRIO3GPU_SPECULATE"]
-        else:
-            os.environ["PRIO3GPU_SPECULATE"] = old
+    v = Prio3Gpu(c["kind"], bytes(range(16)), bits=c["bits"], length=c["length"],
+                 chunk_length=c["chunk"])
+    v.set_option("speculate", int(speculate))
+    return v
 
 
 def _meas(name, n, rng):
@@ -51,19 +43,14 @@ def _plain(name, meas, sel):
     return int(m[:, 0].sum())
 
 
-@pytest.mark.parametrize("helper_mode", ["fused", "fallback", "twopass"])
-def test_sumvec_8_1000_multichunk_fold_bytes_vs_c_restatement(helper_mode, monkeypatch):
+def test_sumvec_8_1000_multichunk_fold_bytes_vs_c_restatement():
     """The headline config at a size that reaches the multi-chunk speculative fold (WCH = 32 waves
     = 2,048 reports per chunk, engine.hip launch_accumulate): 4,200 SumVec(8, 1000) reports,
     slot 0 over 36 whole waves (two speculative chunks), slot 1 over 28 waves, one mixed-slot wave
     (direct path) and a partial last wave of 40 rows on slot 2; six reports tampered inside the
     column-summed window (element 500) so k_accum_spec must subtract their rows.  Both
-    aggregators' aggregate shares and counts per slot must equal the C restatement's bytes, with
-    the helper's sponges fused (k_helper_sponge), forced onto its exact fallback, or two-pass."""
+    aggregators' aggregate shares and counts per slot must equal the C restatement's bytes."""
     from janus_amd.prio3 import Prio3Gpu
-    monkeypatch.setenv("PRIO3GPU_HELPER_SPONGE", "0" if helper_mode == "twopass" else "1")
-    if helper_mode == "fallback":
-        monkeypatch.setenv("PRIO3GPU_TEST_FALLBACK", "1")
     from oracle import prio3 as O
     from oracle.ref import Prio3Ref
     n = 4200

@@ -8,7 +8,7 @@ reports.  Two checks close that gap:
     are dense in non-canonical chunks and edge values (p - 1, p, 2^128 - 1, high word exactly
     2^64 - 28), against the oracle's `field_vec_from_stream` on the same bytes, with and without
     the forced exact path;
-  * PRIO3GPU_EXACT_SQUEEZE=1 forces the exact path in every real XOF kernel (query randomness,
+  * the engine option exact_squeeze = 1 forces the exact path in every real XOF kernel (query randomness,
     helper expansion, joint randomness, shard): every golden config must stay byte-identical.
 """
 import ctypes
@@ -143,12 +143,12 @@ def test_crafted_stream_overrun_is_an_error():
 @pytest.mark.parametrize("name", ["count", "sum8", "sum32", "sumvec_small", "countvec15", "hist4",
                                   "hist256", "sumvec_8_1000", "fp16_3", "fp32_5", "fp64_4",
                                   "fp16_300", "fp16_5000"])
-def test_exact_squeeze_forced_transcript_bit_exact(name, monkeypatch):
-    monkeypatch.setenv("PRIO3GPU_EXACT_SQUEEZE", "1")
+def test_exact_squeeze_forced_transcript_bit_exact(name):
     from tests.test_gpu_parity import batch, gpu_vdaf
     from tests.reports import meas_array
     b = batch(name)
-    v = gpu_vdaf(b)  # created after the switch is set: the context reads it
+    v = gpu_vdaf(b)
+    v.set_option("exact_squeeze", 1)
     ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
     lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
     hp, hst = v.prepare_init(hs, b.nonces, b.public, b.helper_in)

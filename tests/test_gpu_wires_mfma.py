@@ -1,6 +1,7 @@
-"""k_flp_wires_mfma (byte-limb convolution on v_mfma_i32_32x32x32_i8, janus_amd/csrc/wires_mfma.h)
-against the VALU wire pass k_flp_wires (PRIO3GPU_WIRES_MFMA=0), which the oracle transcripts pin
-(tests/test_gpu_parity.py runs every SumVec config with chunk > 64 through the MFMA kernel).
+"""k_flp_wires_mfma (byte-limb convolution on v_mfma_i32_32x32x32_i8, janus_amd/csrc/wires_mfma.h;
+chunk > 64) and k_flp_wires_cols (lane per column; chunk <= 64) against the VALU wire pass
+k_flp_wires (engine options wires_mfma = wires_cols = 0), which the oracle transcripts pin
+(tests/test_gpu_parity.py runs every config through the default kernels).
 
 Here: many random leader shares per shape, so the exact-integer path sees thousands of random
 weights and elements (top bytes near 0xFF, all-zero and all-0xFF words, padding in the last call,
@@ -18,7 +19,7 @@ SHAPES = [(2, 8, 1000, 89),   # 90 calls, last call 79 of 89 columns; 3 tiles, 2
           (2, 1, 1000, 128),  # 8 calls, 4 full tiles (no spare column)
           (2, 3, 300, 65),    # 14 calls, a 1-column last tile
           (2, 2, 3000, 300),  # 20 calls, 10 tiles, 4 waves looping over them
-          # short rows (chunk 8..32): a wave per report, 4 reports per block
+          # short rows (chunk <= 64): k_flp_wires_cols
           (3, 0, 256, 16),    # Histogram256 (BASELINE config C): 16 calls; v needs sum x
           (3, 0, 100, 10),    # Histogram, 10 calls
           (2, 4, 100, 32),    # 13 calls (odd), a full 32-column tile
@@ -26,10 +27,13 @@ SHAPES = [(2, 8, 1000, 89),   # 90 calls, last call 79 of 89 columns; 3 tiles, 2
 
 
 def _vdaf(kind, bits, length, chunk, monkeypatch, mfma, vk=bytes(range(16))):
+    """mfma: the default wire passes; else the VALU k_flp_wires for every shape."""
     from janus_amd.prio3 import Prio3Gpu
-    monkeypatch.setenv("PRIO3GPU_WIRES_MFMA", "1" if mfma else "0")
-    monkeypatch.setenv("PRIO3GPU_WIRES_MFMA_SHORT", "1" if mfma else "0")
-    return Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk)
+    v = Prio3Gpu(kind, vk, bits=bits, length=length, chunk_length=chunk)
+    if not mfma:
+        v.set_option("wires_mfma", 0)
+        v.set_option("wires_cols", 0)
+    return v
 
 
 def _random_shares(rng, n, s, meas_len, extremes):

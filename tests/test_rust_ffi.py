@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "prio3gpu.h")
 FFI = os.path.join(ROOT, "rust", "aggregator", "src", "gpu", "ffi.rs")
 
-C_BASE = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u64",
+C_BASE = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u64", "int64_t": "i64",
           "size_t": "usize", "int": "c_int", "double": "f64", "void": "c_void", "char": "c_char"}
 
 

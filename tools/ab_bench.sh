@@ -1,16 +1,18 @@
 #!/bin/bash
 # A/B of bench.py variants on one box, each run under its own time limit; stops at the first
-# failure (GPU fault, abort, timeout).  Each argument is  LABEL:LIB:BENCH-ARGS  where LIB is a
+# failure (GPU fault, abort, timeout).  Each argument is  LABEL|LIB|ENV|BENCH-ARGS  where LIB is a
 # variant library name (tools/build_variant.sh NAME -> janus_amd/lib/libprio3gpu_NAME.so) or
-# "base", e.g.
-#   bash tools/ab_bench.sh "ov0:base:--overlap 0" "ov2:base:--overlap 2" "ov2p:prio2:--overlap 2"
+# "base", ENV is "-" or space-separated VAR=value settings for that run only, e.g.
+#   bash tools/ab_bench.sh "ov0|base|-|--overlap 0" "ov2cap|base|PRIO3GPU_JR_LDS=65536|--overlap 2"
 # Output: gpurun_out/ab_LABEL.log, one summary line per run on stdout.
 O=gpurun_out; mkdir -p $O
 COMMON="--steps 6 --warmup 2 --cpu-baseline 0 --hpke 0 --helper-only 0"
 for spec in "$@"; do
-  label=${spec%%:*}; rest=${spec#*:}; libn=${rest%%:*}; args=${rest#*:}
-  if [ "$libn" = base ]; then unset PRIO3GPU_LIB; else export PRIO3GPU_LIB=janus_amd/lib/libprio3gpu_$libn.so; fi
-  timeout -k 10 300 python -u bench.py $COMMON $args > $O/ab_$label.log 2>&1
+  IFS='|' read -r label libn envs args <<< "$spec"
+  vars=()
+  [ "$libn" != base ] && vars+=("PRIO3GPU_LIB=janus_amd/lib/libprio3gpu_$libn.so")
+  [ "$envs" != "-" ] && vars+=($envs)
+  env "${vars[@]}" timeout -k 10 300 python -u bench.py $COMMON $args > $O/ab_$label.log 2>&1
   rc=$?
   python - "$O/ab_$label.log" "$label" "$rc" <<'PY'
 import json, sys
