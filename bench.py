@@ -258,8 +258,10 @@ def main():
                     help="CPU-baseline threads (0: the host CPUs this process may use)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="1: leader and helper on separate contexts/streams, prepare_init "
-                         "concurrent; 2: pipelined schedule (each batch's HBM-bound FLP query "
-                         "under the other aggregator's Keccak, async contexts, see DESIGN §5)")
+                         "concurrent; 2: pipelined schedule (each batch's FLP query under the "
+                         "other aggregator's Keccak, async contexts, see DESIGN §5); 3: the same "
+                         "with the latency-bound FLP weights kept out from under the Keccak "
+                         "(only the HBM-bound wire pass overlaps)")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -485,8 +487,8 @@ def main():
     #   A waits mB2; A: leader prepare_next + accumulate(i), report meta
     # Both streams are drained (and, N > 1, the partials merged) at the end of the run.
     pipe = None
-    if args.overlap == 2:
-        assert W == 1, "--overlap 2 runs one job worker"
+    if args.overlap in (2, 3):
+        assert W == 1, "--overlap 2/3 runs one job worker"
         wk = workers[0]
         A, Bv = wk.v, wk.hv
         A.set_async(True)
@@ -504,11 +506,18 @@ def main():
             v._ctx, st._h, wk.n, p["nonces"], p["pub"], inp, P(status)), "prepare_init_xof")
         query = lambda v, st, status, out: check(L.prio3gpu_prepare_init_query(
             v._ctx, st._h, wk.n, out, P(status)), "prepare_init_query")
+        weights = lambda v, st, status: check(L.prio3gpu_prepare_init_weights(
+            v._ctx, st._h, wk.n, P(status)), "prepare_init_weights")
+        w3 = args.overlap == 3
         xof(A, ls[0], lst[0], p["lin"])
         for i in range(k_steps):
             cur, nxt = i % 2, (i + 1) % 2
+            if w3:  # A's weights(i) before B's Keccak starts
+                weights(A, ls[cur], lst[cur])
             Bv.wait_for(A)
             xof(Bv, wk.hs, d_hst, p["hin"])
+            if w3:  # B's weights(i) before A's next Keccak starts
+                weights(Bv, wk.hs, d_hst)
             mB = Bv.mark()
             query(A, ls[cur], lst[cur], p["lprep"])
             mA = A.mark()
@@ -550,7 +559,7 @@ def main():
                 comm.allreduce(wk.hv, wk.hpart, wk.hagg)
 
     d_hprep2 = (torch.empty((B, s.prep_share), dtype=torch.uint8, device=dev)
-                if args.overlap == 2 else None)
+                if args.overlap in (2, 3) else None)
     if pipe is not None:
         run_pipelined(max(1, args.warmup))
     else:
@@ -772,7 +781,7 @@ def main():
                     nlaunch * s.meas_len * s.field_size if dname == "k_jr" else
                     nlaunch * (s.meas_len + s.proof_len) * s.field_size if dname == "k_expand"
                     else None)}
-    elif dname in ("k_flp_query_lane", "k_flp_query_sum"):  # the whole FLP query of Count / Sum
+    elif dname == "k_flp_query_lane":  # the whole FLP query of Count / Sum in one kernel
         mults = flp_mults_per_report(s, kind)
         per_mul = OPS_PER_F128_MUL if s.field_size == 16 else OPS_PER_F64_MUL
         achieved = mults * per_mul * nlaunch / avg_launch_s / 1e12

@@ -138,7 +138,6 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
  *   "speculate"     1: accumulate from k_jr's per-wave column sums; 0: direct accumulation
  *   "wires_mfma"    1: SumVec (chunk > 64) wire pass on the matrix cores; 0: VALU k_flp_wires
  *   "wires_cols"    1: chunk <= 64 lane-per-column wire pass; 0: VALU k_flp_wires
- *   "sum_split"     1: Sum's FLP query on two waves per 64 reports; 0: one lane per report
  *   "fused_helper"  1: FixedPoint helper XOF pipeline (k_helper_xof); 0: exact two-pass path
  *   "jr_ring"       1: FixedPoint leader joint-rand part via k_jr_ring; 0: k_jr
  *   "spread"        1: latency-bound sponge launches take one CU per workgroup
@@ -220,6 +219,11 @@ int prio3gpu_prepare_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const
 int prio3gpu_prepare_init_xof(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n,
                               const uint8_t* nonces, const uint8_t* public_shares,
                               const uint8_t* input_shares, uint8_t* status);
+/* Optional step between the two: the latency-bound first half of the FLP query (ParallelSum types:
+ * k_flp_weights -- Lagrange weights, gadget poly at t, circuit output), so a scheduler can keep it
+ * out from under another context's sponge kernels and overlap only the HBM-bound wire pass
+ * (prio3gpu_prepare_init_query then runs just that).  A no-op for Count / Sum / FixedPoint. */
+int prio3gpu_prepare_init_weights(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, uint8_t* status);
 int prio3gpu_prepare_init_query(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n,
                                 uint8_t* out_prep_shares, uint8_t* status);
 

@@ -108,6 +108,7 @@ def _declare(lib):
         "prio3gpu_ctx_wait_mark": (c.c_int, [P, P, c.c_int]),
         "prio3gpu_prepare_init_xof": (c.c_int, [P, P, c.c_size_t, u8p, u8p, u8p, u8p]),
         "prio3gpu_prepare_init_query": (c.c_int, [P, P, c.c_size_t, u8p, u8p]),
+        "prio3gpu_prepare_init_weights": (c.c_int, [P, P, c.c_size_t, u8p]),
         "prio3gpu_ctx_sizes": (c.c_int, [P, P]),
         "prio3gpu_ctx_sync": (c.c_int, [P]),
         "prio3gpu_ctx_stream": (P, [P]),
@@ -191,7 +192,7 @@ EXPORTED = [
     "prio3gpu_ctx_sync", "prio3gpu_ctx_set_async", "prio3gpu_ctx_set_option", "prio3gpu_ctx_wait",
     "prio3gpu_ctx_mark",
     "prio3gpu_ctx_wait_mark",
-    "prio3gpu_prepare_init_xof", "prio3gpu_prepare_init_query",
+    "prio3gpu_prepare_init_xof", "prio3gpu_prepare_init_query", "prio3gpu_prepare_init_weights",
     "prio3gpu_ctx_stream", "prio3gpu_state_create", "prio3gpu_state_destroy",
     "prio3gpu_state_set_input_pitch",
     "prio3gpu_agg_create", "prio3gpu_agg_destroy", "prio3gpu_agg_reset", "prio3gpu_agg_read",

@@ -147,7 +147,7 @@ enum KernelId {
   KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE, KID_SHARD_SEEDS,
   KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META, KID_REPORT_META_FOLD,
   KID_SHARD_NORM, KID_JR_RING, KID_FLP_QUERY_LANE, KID_FLP_WIRES_COLS, KID_FLP_WIRES_MFMA,
-  KID_FLP_QUERY_SUM, KID_COUNT
+  KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_helper_xof", "k_jr", "k_flp_weights", "k_flp_wires",
@@ -155,7 +155,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge", "k_out_shares", "k_merge",
     "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove", "k_shard_proof", "k_report_meta",
     "k_report_meta_fold", "k_shard_norm", "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols",
-    "k_flp_wires_mfma", "k_flp_query_sum"};
+    "k_flp_wires_mfma"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -199,7 +199,6 @@ struct prio3gpu_ctx {
   bool jr_ring = true;       // "jr_ring": FixedPoint leader joint-rand part via k_jr_ring
   bool wires_mfma = true;    // "wires_mfma": SumVec chunk > 64 wire pass on the matrix cores
   bool wires_cols = true;    // "wires_cols": chunk <= 64 lane-per-column wire pass
-  bool sum_split = true;     // "sum_split": Sum's FLP query on two waves per 64 reports
   size_t expand_lds = 0;     // "expand_lds": dynamic LDS per k_expand block (occupancy cap)
   size_t jr_lds = 0;         // "jr_lds": dynamic LDS per k_jr block (occupancy cap)
   uint32_t cus = 0;          // compute units of the device
@@ -258,6 +257,7 @@ struct prio3gpu_state {
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
   CRows proof_rows{nullptr, 0};  // proof shares (prepare_init_xof -> prepare_init_query)
   bool xof_done = false;         // the XOF phase ran; the query phase is due
+  bool weights_done = false;     // ParallelSum: k_flp_weights of the query phase ran already
   // speculative accumulation: per-wave column sums of meas-share words, written by k_jr
   DevBuf spec_lo, spec_cy;
   bool spec_ok = false;
@@ -584,7 +584,8 @@ int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, 
 }
 
 template <class FO>
-int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_status);
+int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_status,
+                      bool weights_only = false);
 
 // Row pitch of a state's input shares: the caller's (prio3gpu_state_set_input_pitch) or packed.
 size_t input_pitch(const prio3gpu_state* st) {
@@ -665,6 +666,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
       st->proof_rows = CRows{po.base, po.stride};
       st->n = n;
       st->xof_done = true;
+      st->weights_done = false;
       return 0;
     }
     {
@@ -711,42 +713,58 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
   st->proof_rows = proof;
   st->n = n;
   st->xof_done = true;
+  st->weights_done = false;
   return 0;
 }
 
 // ParallelSum types (SumVec, Histogram, Field128): the FLP query in two kernels -- the Lagrange
 // weights and the rest of the verifier except the wires (k_flp_weights: lane per report,
 // latency-bound), then the wire pass over the measurement share (HBM streaming).
+// weight rows (row-major), then k_flp_weights' element-major scratch (block prefix products)
+WMat psum_wrows(const prio3gpu_state* st) {
+  const Cfg& g = st->ctx->cfg;
+  return WMat{st->w.u8(), (size_t)flp_w_len(g) * g.es, (size_t)g.es};
+}
+
+int launch_psum_weights(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows proof,
+                        uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  const uint32_t N = (uint32_t)n;
+  uint8_t* wscr = st->w.u8() + (size_t)N * flp_w_len(g) * g.es;
+  PROF(KID_FLP_WEIGHTS);
+  hipLaunchKernelGGL(k_flp_weights, grid1(n, kFwThreads), dim3(kFwThreads), 0, c->stream, g, N,
+                     proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * g.es},
+                     CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
+                     psum_wrows(st), wscr);
+  HIPCHK(hipGetLastError());
+  st->weights_done = true;
+  return 0;
+}
+
 int launch_psum_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, CRows proof,
                       uint8_t* d_status) {
   const Cfg& g = c->cfg;
   const uint32_t es = g.es;
   const uint32_t N = (uint32_t)n;
-  // weight rows (row-major), then k_flp_weights' element-major scratch (calls x n entries)
-  const WMat wrows{st->w.u8(), (size_t)flp_w_len(g) * es, (size_t)es};
-  uint8_t* wscr = st->w.u8() + (size_t)N * flp_w_len(g) * es;
+  if (!st->weights_done) CHK(launch_psum_weights(c, st, n, proof, d_status));
+  st->weights_done = false;
+  const WMat wrows = psum_wrows(st);
   const CRows jr{st->jr.u8(), (size_t)g.jr_len * es};
   const Rows prep{st->prep.u8(), g.prep_share_len};
-  {
-    PROF(KID_FLP_WEIGHTS);
-    hipLaunchKernelGGL(k_flp_weights, grid1(n, kFwThreads), dim3(kFwThreads), 0, c->stream, g, N,
-                       proof, CRows{st->t.u8(), 16}, jr, CRows{st->part.u8(), 16}, prep, d_status,
-                       wrows, wscr);
-  }
   if (g.chunk <= 64 && c->wires_cols) {
     // G = next_pow2(chunk) lanes per report, lane = column (Histogram, small SumVec/CountVec)
     uint32_t lg = 0;
     while ((1u << lg) < g.chunk) ++lg;
     PROF(KID_FLP_WIRES_COLS);
     hipLaunchKernelGGL(k_flp_wires_cols, grid1((size_t)N << lg, 256), dim3(256), 0, c->stream, g, N,
-                       lg, meas, wrows, jr, prep, d_status);
+                       lg, meas, proof, wrows, jr, prep, d_status);
   } else if (c->wires_mfma && g.kind == KIND_SUMVEC && g.chunk > 64 && g.calls <= kWmMaxCalls &&
              wires_mfma_e_bytes(g.calls) + 16 <= 64 * 1024) {
     // byte-limb convolution on v_mfma_i32_32x32x32_i8 (wires_mfma.h): a wave per 32 columns
     const uint32_t nwv = std::min(4u, (g.chunk + 31) / 32);
     PROF(KID_FLP_WIRES_MFMA);
     hipLaunchKernelGGL(k_flp_wires_mfma, dim3(N), dim3(64 * nwv), wires_mfma_e_bytes(g.calls) + 16,
-                       c->stream, g, N, meas, wrows, jr, prep, d_status);
+                       c->stream, g, N, meas, proof, wrows, prep, d_status);
   } else {
     // the VALU wire pass: block per report, (column, row group) slots; short reports get >= 4
     // rows per thread (Histogram256: H 16 -> 4 took 18.0 -> 6.1 ms/step,
@@ -771,7 +789,7 @@ int launch_psum_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas,
     }
     PROF(KID_FLP_WIRES);
     hipLaunchKernelGGL(k_flp_wires<Field128Ops>, dim3(N), dim3(nthr), lds2, c->stream, g, N, dims,
-                       meas, wrows, jr, prep, d_status);
+                       meas, proof, wrows, jr, prep, d_status);
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -779,7 +797,8 @@ int launch_psum_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas,
 
 // prepare_init, second phase: the FLP query over the shares the first phase left in the state.
 template <class FO>
-int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_status) {
+int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_status,
+                      bool weights_only) {
   const Cfg& g = c->cfg;
   const uint32_t es = g.es;
   const uint32_t N = (uint32_t)n;
@@ -787,6 +806,13 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
   if (!st->xof_done || st->n != n) {
     set_err("prepare_init query phase without its XOF phase over the same %zu reports", n);
     return PRIO3GPU_E_ARG;
+  }
+  const bool psum = (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM);
+  if (weights_only) {  // the latency-bound first half of a ParallelSum query; others: nothing yet
+    if constexpr (FO::ES == 16) {
+      if (psum && !st->weights_done) CHK(launch_psum_weights(c, st, n, proof, d_status));
+    }
+    return 0;
   }
   st->xof_done = false;
   if constexpr (FO::ES == 16) {
@@ -798,24 +824,12 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
   // FLP query: block per report.  ParallelSum types (SumVec, Histogram) split it in two: the
   // weights (power tables, NTTs, gadget outputs; latency-bound, 2 waves) and the wire pass over
   // the measurement share (HBM streaming, many blocks in flight).
-  const bool psum = (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM);
   if constexpr (FO::ES == 16) {
     if (psum) return launch_psum_query(c, st, n, meas, proof, d_status);
   }
   if (g.kind != KIND_COUNT && g.kind != KIND_SUM) {
     set_err("no FLP query for VDAF kind %u", g.kind);
     return PRIO3GPU_E_ARG;
-  }
-  if constexpr (FO::ES == 16) {
-    if (g.kind == KIND_SUM && c->sum_split && g.arity == 1) {
-      PROF(KID_FLP_QUERY_SUM);
-      hipLaunchKernelGGL(k_flp_query_sum, grid1(n, kFqsReports), dim3(2 * kFqsReports), 0,
-                         c->stream, g, N, meas, proof, CRows{st->t.u8(), 16},
-                         CRows{st->jr.u8(), (size_t)g.jr_len * es}, CRows{st->part.u8(), 16},
-                         Rows{st->prep.u8(), g.prep_share_len}, d_status);
-      HIPCHK(hipGetLastError());
-      return 0;
-    }
   }
   {
     PROF(KID_FLP_QUERY_LANE);
@@ -1209,7 +1223,7 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   rc |= st->msg.ensure(N * 16);
   rc |= st->status.ensure(N);
   if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM)
-    rc |= st->w.ensure(N * (size_t)(flp_w_len(g) + g.calls) * g.es);  // rows + scratch
+    rc |= st->w.ensure(N * (size_t)(flp_w_len(g) + flp_scratch_len(g)) * g.es);  // rows + scratch
   if (g.kind == KIND_FPVEC) {
     rc |= st->w.ensure(N * (size_t)fpv_w_layout(g).len * 16);
     rc |= st->fpart.ensure(N * (size_t)fpv_rows(g) * g.chunk * 32);
@@ -1519,6 +1533,20 @@ int prio3gpu_prepare_init_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n,
   return finish_call(c, {out_prep_shares, status});
 }
 
+int prio3gpu_prepare_init_weights(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* status) {
+  CHK(check_state(c, st, n));
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  uint8_t* d_status;
+  CHK(stage_status(c, st->status, status, n, &d_status));
+  if (is_f64(c))
+    CHK(launch_prep_query<Field64Ops>(c, st, n, d_status, true));
+  else
+    CHK(launch_prep_query<Field128Ops>(c, st, n, d_status, true));
+  CHK(copy_out(c, status, d_status, n));
+  return finish_call(c, {status});
+}
+
 int prio3gpu_ctx_set_async(prio3gpu_ctx* c, int on) {
   if (!c) return PRIO3GPU_E_ARG;
   c->async_mode = on != 0;
@@ -1544,8 +1572,7 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
     c->wires_mfma = on;
   } else if (k == "wires_cols") {
     c->wires_cols = on;
-  } else if (k == "sum_split") {
-    c->sum_split = on;
+
   } else if (k == "expand_lds" || k == "jr_lds") {
     if (value < 0 || value > 160 * 1024) {
       set_err("option %s: %lld bytes is outside [0, 163840]", name, (long long)value);

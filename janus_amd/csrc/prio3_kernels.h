@@ -781,11 +781,40 @@ struct FlpDims {
   uint32_t rp_len;  // entries of the r-power table RP
 };
 
-// W row written by k_flp_weights (ParallelSum types) and read by the wire passes:
-//   MM[1..calls] | LM[1..calls] | RP[1..c] | B0[c] = L0 s_2j | B1[c] = L0 s_2j+1 - (1/2) sum L_k | gsum
-// (k_flp_weights also appends SMM = sum_k MM[k] and SLM = sum_k LM[k] mod p: k_flp_wires_mfma's
-// offset correction, wires_mfma.h)
-__host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + 3 * cfg.chunk + 3; }
+// W row written by k_flp_weights (ParallelSum types) and read by the wire passes (Montgomery form):
+//   MM[k] = L_k r^(c(k-1)) | LM[k] = L_k (k = 1..calls) | RP[j] = r^(j+1) (j < c) |
+//   L0 | HL = (1/2) sum_(k>=1) L_k | gsum (circuit output before the range/sum mix) |
+//   SMM = sum_k MM[k] | SLM = sum_k LM[k]   (mod p: k_flp_wires_mfma's offset correction)
+// The wire passes finish  wire_2j = L0 s_2j + RP[j] a_j,  wire_2j+1 = L0 s_2j+1 - HL + b_j  from the
+// proof share's wire seeds s themselves (and check them canonical).
+struct WRow {
+  uint32_t C, c;
+  DEVI explicit WRow(const Cfg& cfg) : C(cfg.calls), c(cfg.chunk) {}
+  DEVI uint32_t mm(uint32_t k0) const { return k0; }  // k0 = k - 1
+  DEVI uint32_t lm(uint32_t k0) const { return C + k0; }
+  DEVI uint32_t rp(uint32_t j) const { return 2 * C + j; }
+  DEVI uint32_t l0() const { return 2 * C + c; }
+  DEVI uint32_t hl() const { return 2 * C + c + 1; }
+  DEVI uint32_t gsum() const { return 2 * C + c + 2; }
+  DEVI uint32_t smm() const { return 2 * C + c + 3; }
+  DEVI uint32_t slm() const { return 2 * C + c + 4; }
+};
+__host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + cfg.chunk + 5; }
+// entries of k_flp_weights' element-major scratch per report: the prefix product at the start of
+// every 8-call block of the batched inversion
+__host__ __device__ inline uint32_t flp_scratch_len(const Cfg& cfg) { return (cfg.calls + 7) / 8; }
+
+// Wire-seed terms of column j (wire_2j, wire_2j+1 without the measurement sums): L0 s_2j and
+// L0 s_2j+1 - HL, from the proof share's seeds; `bad` if a seed is not canonical.
+DEVI void wire_seed_terms(const WMat& wm, const WRow& W, uint32_t r, const uint8_t* seeds,
+                          uint32_t j, F128& t0, F128& t1, bool& bad) {
+  using FO = Field128Ops;
+  const F128 l0 = FO::load(wm.el(r, W.l0()));
+  const F128 s0 = FO::load(seeds + (size_t)(2 * j) * 16), s1 = FO::load(seeds + (size_t)(2 * j + 1) * 16);
+  bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
+  t0 = FO::mul(l0, s0);
+  t1 = FO::sub(FO::mul(l0, s1), FO::load(wm.el(r, W.hl())));
+}
 
 // ------------------------------------------------------------------------------------------------
 // FLP query for Count (Mul, 1 call) and Sum (PolyEval(x^2 - x), `bits` calls), one LANE per report:
@@ -1040,160 +1069,6 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
 }
 
 // ------------------------------------------------------------------------------------------------
-// FLP query for Sum (Field128), the same arithmetic as k_flp_query_lane split over TWO waves per 64
-// reports, so each wave keeps about half the live state (more waves per SIMD hide the Montgomery
-// chains' latency, which bounds the one-lane form at 2 waves/SIMD):
-//   wave 0 ("H"): Horner on p(t) = sum_i (c_i + t^m c_(i+m)) t^i and the wire fraction
-//                 N/D = sum_(k=0..calls) alpha^k x_k / (t - alpha^k) (k = 0: the proof seed);
-//   wave 1 ("V"): the gadget-output fraction  v = sum_(i<m) F_i G(r alpha^i)  (F = the gadget poly
-//                 folded mod x^m - 1, G(y) = y (y^calls - 1)/(y - 1)), whose numerator and
-//                 denominator it hands to wave 0 through LDS;
-// wave 0 then inverts both denominators with one inversion and writes the prep share.  Products
-// issue as hazard-free triples (mont_mul3).  Bit-identical to k_flp_query_lane (same field values).
-// ------------------------------------------------------------------------------------------------
-constexpr uint32_t kFqsReports = 64;
-
-__global__ void __launch_bounds__(2 * kFqsReports) k_flp_query_sum(Cfg cfg, uint32_t n, CRows meas,
-                                                                   CRows proof, CRows tq, CRows jr,
-                                                                   CRows part, Rows out_prep,
-                                                                   uint8_t* status) {
-  using FO = Field128Ops;
-  using T = F128;
-  __shared__ __attribute__((aligned(16))) T xch[3][kFqsReports];  // V -> H: vn, vd, extra
-  const uint32_t lane = threadIdx.x & 63u, role = threadIdx.x >> 6;  // role wave-uniform
-  const uint32_t r = blockIdx.x * kFqsReports + lane;
-  const bool live = r < n && status[r] == ST_OK;
-  const uint32_t rr = r < n ? r : n - 1u;  // dead lanes compute on a valid row, store nothing
-  const uint32_t m = cfg.m, calls = cfg.calls, gp_len = cfg.gp_len;
-  const uint8_t* pr = proof.at(rr);
-  const uint8_t* gp = pr + (size_t)cfg.arity * 16;  // gadget poly coefficients (arity 1)
-  const T one = FO::one_mont();
-  const bool half = 2u * calls == m;  // power-of-two bits: y^calls = +-r^calls
-  if (role == 1) {
-    // ---- V: r^m, r^calls, then the fraction over i = m-1 .. 0 ----
-    const T rm = FO::to_mont(FO::load(jr.at(rr)));
-    T rmm = rm, rc = one, b = rm;
-    for (uint32_t q = 0; q < cfg.logm; ++q) {
-      if ((calls >> q) & 1u) rc = FO::mul(rc, b);
-      T idle;
-      mul3<FO>(rmm, rmm, b, b, one, one, rmm, b, idle);
-    }
-    T vn = FO::zero(), vd = one, extra = FO::zero();
-    auto fcoef = [&](uint32_t i) {
-      const T ci = FO::load(gp + (size_t)i * 16);
-      return i + m < gp_len ? FO::add(ci, FO::load(gp + (size_t)(i + m) * 16)) : ci;
-    };
-    if (!FO::eq(rmm, one)) {
-      const T ycm_even = FO::sub(rc, one), ycm_odd = FO::sub(FO::sub(FO::zero(), rc), one);
-      T y = FO::mul(rm, ld_tw<FO>(cfg, m - 1u));
-      T um1 = FO::zero();  // u - 1 for the current i (non-half)
-      if (!half)
-        um1 = FO::sub(FO::mul(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)(m - 1u) * calls) % m))), one);
-      for (uint32_t i = m - 1;; --i) {
-        const T f = fcoef(i);
-        const T e = FO::sub(y, one);
-        const T gm = half ? ((i & 1u) ? ycm_odd : ycm_even) : um1;
-        const uint32_t in = i ? i - 1u : 0u;
-        T yf, g, yn, yfg, vde, vne;
-        mul3<FO>(y, f, gm, vd, rm, ld_tw<FO>(cfg, in), yf, g, yn);
-        if (!half) {  // next iteration's u - 1 (an idle pair: only configs with bits != 2^k)
-          T un, i1, i2;
-          mul3<FO>(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)in * calls) % m)), one, one, one, one,
-                   un, i1, i2);
-          um1 = FO::sub(un, one);
-        }
-        mul3<FO>(yf, g, vd, e, vn, e, yfg, vde, vne);
-        vn = FO::add(vne, yfg);
-        vd = vde;
-        y = yn;
-        if (i == 0) break;
-      }
-    } else {  // r^m == 1 (probability ~m / p): some y_i == 1, where G = calls
-      const T calls_m = FO::to_mont(FO::from_u32(calls));
-      for (uint32_t i = m; i-- > 0;) {
-        const T f = fcoef(i);
-        const T y = FO::mul(rm, ld_tw<FO>(cfg, i));
-        if (FO::is_zero(FO::sub(y, one))) {
-          extra = FO::add(extra, FO::mul(calls_m, f));
-        } else {
-          const T e = FO::sub(y, one);
-          const T yc = FO::mul(rc, ld_tw<FO>(cfg, (uint32_t)(((uint64_t)i * calls) % m)));
-          const T bb = FO::mul(FO::mul(y, f), FO::sub(yc, one));
-          vn = FO::add(FO::mul(vn, e), FO::mul(bb, vd));
-          vd = FO::mul(vd, e);
-        }
-      }
-    }
-    xch[0][lane] = vn;
-    xch[1][lane] = vd;
-    xch[2][lane] = extra;
-    __syncthreads();
-    return;
-  }
-  // ---- H: t^m, Horner and the wire fraction over i = m-1 .. 0 ----
-  const uint8_t* xr = meas.at(rr);
-  bool bad = false;
-  const T tm = FO::to_mont(FO::load(tq.at(rr)));
-  T tmm = tm;
-  for (uint32_t i = 0; i < cfg.logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
-  const bool root = FO::eq(tmm, one);
-  const T cm = FO::mul(FO::sub(tmm, one), ld_tw<FO>(cfg, m));  // (t^m - 1)/m, Montgomery
-  const T s0 = FO::load(pr);
-  bad |= !FO::is_canonical(s0);
-  T pt = FO::zero(), nw0 = FO::zero(), dw = one;
-  for (uint32_t i = m - 1;; --i) {
-    const T ci = FO::load(gp + (size_t)i * 16);
-    const T ch = i + m < gp_len ? FO::load(gp + (size_t)(i + m) * 16) : FO::zero();
-    bad |= !FO::is_canonical(ci) || !FO::is_canonical(ch);
-    const T twi = ld_tw<FO>(cfg, i);
-    T q, P, a;
-    if (i >= 1 && i <= calls) {
-      const T x = FO::load(xr + (size_t)(i - 1) * 16);
-      bad |= !FO::is_canonical(x);
-      const T d = FO::sub(tm, twi);
-      mul3<FO>(tmm, ch, tm, pt, twi, x, q, P, a);
-      T dwn, adw, nwd;
-      mul3<FO>(dw, d, a, dw, nw0, d, dwn, adw, nwd);
-      nw0 = FO::add(nwd, adw);
-      dw = dwn;
-    } else {
-      T idle;
-      mul3<FO>(tmm, ch, tm, pt, one, one, q, P, idle);
-    }
-    pt = FO::add(P, FO::add(ci, q));
-    if (i == 0) break;
-  }
-  {  // the k = 0 wire term: a = the proof seed
-    const T d = FO::sub(tm, one);
-    T nd, sd, dd;
-    mul3<FO>(nw0, d, s0, dw, dw, d, nd, sd, dd);
-    nw0 = FO::add(nd, sd);
-    dw = dd;
-  }
-  __syncthreads();
-  const T vn = xch[0][lane], vd = xch[1][lane], extra = xch[2][lane];
-  // one inversion for both denominators
-  const T inv = inv_mont<FO>(FO::mul(dw, vd));
-  T dinv, vinv, idle;
-  mul3<FO>(inv, vd, inv, dw, one, one, dinv, vinv, idle);
-  T nd, vv;
-  mul3<FO>(nw0, dinv, vn, vinv, one, one, nd, vv, idle);
-  const T w0 = FO::mul(cm, nd);
-  const T v = FO::add(vv, extra);
-  if (!live) return;
-  uint8_t* outp = out_prep.at(r);
-  FO::store(outp, v);
-  FO::store(outp + 16, w0);
-  FO::store(outp + 32, pt);  // (1 + arity) * 16 with arity 1
-  const uint8_t* pp = part.at(r);
-  uint8_t* dst = outp + (size_t)cfg.verifier_len * 16;
-  st64(dst, ld64(pp));
-  st64(dst + 8, ld64(pp + 8));
-  if (bad) status[r] = ST_INVALID_MESSAGE;
-  else if (root) status[r] = ST_VDAF_PREP_ERROR;
-}
-
-// ------------------------------------------------------------------------------------------------
 // Cross-lane helpers for Field elements.
 // ------------------------------------------------------------------------------------------------
 template <class FO>
@@ -1225,39 +1100,26 @@ DEVI typename FO::T sel(bool c, const typename FO::T& a, const typename FO::T& b
 }
 
 // ------------------------------------------------------------------------------------------------
-// FLP query, ParallelSum types, first half, one LANE per report (Field128).  Same outputs as the
-// round-1 wave-per-report form (since removed), with about half its multiplications and no
-// cross-lane arithmetic:
+// FLP query, ParallelSum types, first half, one LANE per report (Field128):
 //   * Lagrange weights L_k(t) = (alpha^k/m) (t^m - 1) / (t - alpha^k), k = 0..calls, from ONE
-//     batched inversion (Montgomery's trick: prefix products of d_k = t - alpha^k parked in an
-//     element-major scratch, one x^(p-2), a backward pass); t^m - 1 is folded into the inverse,
-//     so each weight costs four multiplications;
-//   * p(t) by three Horner chains in t^3, the gadget-output sum sum_d c_d S[d mod m] as a lazily
-//     reduced dot product;
-//   * the serial chains (backward pass, Horner) and the seed products issue as hazard-free
-//     Field128 triples (mont_mul3): 4.76 -> 4.22 ms/step on Histogram(256), 7.23 -> 6.85 on SumVec;
-//   * r^(j+1), MM[k] = LM[k] r^(c(k-1)), B0/B1 by running products.
-// Table entries (alpha^k, alpha^k/m, S_i) are wave-uniform (scalar loads).  Memory is moved
-// coalesced in both directions through two per-wave LDS windows of 8 elements x 64 reports (slot
-// 8q + (u ^ ((q >> 1) & 7)) holds element u of report q: each lane's ds_read/write_b128 of its own
-// row is bank-conflict-free, and 8 lanes cover one report's 128 contiguous bytes):
-//   * the proof share (row-major input) arrives by LDS-DMA, 8 reports x 128 B per instruction,
-//     the next window in flight under the arithmetic of the current one;
-//   * the weight rows (row-major, read per report by k_flp_wires) leave 8 entries at a time.
+//     batched inversion (Montgomery's trick over d_k = t - alpha^k) whose prefix products are kept
+//     only at the start of every 8-call block (element-major scratch, 1/8 of the products) and
+//     recomputed inside a block on the way back; r^c is folded into the same inversion, so
+//     MM[k] = L_k r^(c(k-1)) comes out of the backward pass directly (descending powers);
+//   * RP[j] = r^(j+1) by a running product beside the prefix products;
+//   * p(t) by three Horner chains in t^3 and the gadget-output sum sum_d c_d S[d mod m] as a lazily
+//     reduced dot product, over the gadget-poly part of the proof share only (the wire seeds are
+//     read by the wire passes, which finish wire_2j = L0 s_2j + ..., see WRow);
+//   * serial chains issue as hazard-free Field128 triples (mont_mul3).
+// Table entries (alpha^k, alpha^k/m, S_i) are wave-uniform (scalar loads).  Memory moves coalesced
+// through two per-wave LDS windows of 8 elements x 64 reports (slot 8q + (u ^ ((q >> 1) & 7))
+// holds element u of report q: each lane's ds_read/write_b128 of its own row is bank-conflict-free,
+// and 8 lanes cover one report's 128 contiguous bytes): the proof share arrives by LDS-DMA, the
+// weight rows leave 8 entries at a time.  Per SumVec(8,1000) report it reads the 255 gadget
+// coefficients (4 KB) and writes MM, LM, RP and five scalars (4.4 KB) plus 0.2 KB of scratch.
 // ------------------------------------------------------------------------------------------------
-#ifndef FLPW_M3_BACK
-#define FLPW_M3_BACK 1
-#endif
-#ifndef FLPW_M3_HORNER
-#define FLPW_M3_HORNER 1
-#endif
-#ifndef FLPW_M3_SEEDS
-#define FLPW_M3_SEEDS 1
-#endif
-// A/B knob: wave priority (s_setprio) of the FLP query kernels, for schedules that run them beside
-// the sponge kernels of another batch (bench.py --overlap 2); 0 = default priority.
 #ifndef P3G_FLP_PRIO
-#define P3G_FLP_PRIO 0
+#define P3G_FLP_PRIO 0  // A/B knob: s_setprio of the FLP kernels (schedules that co-run them)
 #endif
 constexpr uint32_t kFwChunk = 8;                  // elements per LDS window
 constexpr uint32_t kFwWin = 64 * kFwChunk * 16;  // bytes per window (one wave)
@@ -1269,30 +1131,31 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
                                                             uint8_t* scr) {
   using FO = Field128Ops;
   using T = F128;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[(kFwThreads / 64) * 2 * kFwWin];
   if constexpr (P3G_FLP_PRIO > 0) __builtin_amdgcn_s_setprio(P3G_FLP_PRIO);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[(kFwThreads / 64) * 2 * kFwWin];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t r0w = blockIdx.x * blockDim.x + 64u * wv;
   if (r0w >= n) return;  // wave-uniform
-  uint8_t* win = lds + wv * 2u * kFwWin;  // proof window
-  uint8_t* wout = win + kFwWin;           // output window
+  uint8_t* win = lds + wv * 2u * kFwWin;  // proof window; later the MM output window
+  uint8_t* wout = win + kFwWin;           // output window (RP, LM)
   const uint32_t r = r0w + lane;
   const bool live = r < n && status[r] == ST_OK;
   const uint64_t livemask = __ballot(live);
   const uint32_t rr = r < n ? r : n - 1u;  // clamped: dead lanes compute on a valid row
   const uint32_t m = cfg.m, logm = cfg.logm, C = cfg.calls, c = cfg.chunk;
-  const uint32_t arity = cfg.arity, total = arity + cfg.gp_len;
-  const uint32_t sw = (lane >> 1) & 7u;   // this lane's swizzle
-  uint8_t* myrow = win + 128u * lane;     // this lane's slots (16 (u ^ sw) within)
-  uint8_t* myout = wout + 128u * lane;
-  auto S = [&](uint32_t k) { return scr + ((size_t)(k - 1u) * n + rr) * 16u; };  // k = 1..C
+  const uint32_t arity = cfg.arity, gp_len = cfg.gp_len;
+  const WRow W(cfg);
+  const uint32_t sw = (lane >> 1) & 7u;  // this lane's swizzle
   const T one = FO::one_mont();
   bool bad = false;
-
-  // proof window <- elements [8 ch, 8 ch + 8) of the wave's 64 rows (LDS-DMA instruction i fills
-  // slots [64i, 64i + 64): report 8i + lane/8, element (lane & 7) ^ swizzle)
+  // block-start prefix products, element-major: entry b holds P_(8b) of report rr
+  auto S = [&](uint32_t b) { return scr + ((size_t)b * n + rr) * 16u; };
+  // this lane's slot u of a window
+  auto put = [&](uint8_t* w, uint32_t u, const T& v) { FO::store(w + 128u * lane + 16u * (u ^ sw), v); };
+  // gadget-poly window <- coefficients [8 ch, 8 ch + 8) of the wave's 64 rows (LDS-DMA instruction
+  // i fills slots [64i, 64i + 64): report 8i + lane/8, element (lane & 7) ^ swizzle)
   auto stage = [&](uint32_t ch) {
-    uint32_t ln;  // opaque copy (see emit)
+    uint32_t ln;  // opaque copy (see flush)
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
     const uint32_t ql = ln >> 3;
 #pragma unroll
@@ -1300,18 +1163,15 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
       const uint32_t q = 8u * i + ql;
       const uint32_t u = (ln & 7u) ^ ((q >> 1) & 7u);
       const uint32_t row = min(r0w + q, n - 1u);
-      const uint32_t e = min(kFwChunk * ch + u, total - 1u);
+      const uint32_t e = arity + min(kFwChunk * ch + u, gp_len - 1u);
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(proof.base + (size_t)row * proof.stride +
                                                           16u * e),
           (__attribute__((address_space(3))) void*)(win + 1024u * i), 16, 0, 0);
     }
   };
-  // weight-row entries [pos, pos + cnt) (cnt <= 8) of every live report of the wave <- v[0..cnt)
-  auto emit = [&](uint32_t pos, const T* v, uint32_t cnt) {
-#pragma unroll
-    for (uint32_t u = 0; u < kFwChunk; ++u)
-      if (u < cnt) FO::store(myout + 16u * (u ^ sw), v[u]);
+  // weight-row entries [pos, pos + cnt) (cnt <= 8) of every live report of the wave <- window w
+  auto flush = [&](uint8_t* w, uint32_t pos, uint32_t cnt) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     uint32_t ln;  // opaque copy: keeps LICM from hoisting 8 row addresses out of the callers' loops
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
@@ -1319,117 +1179,47 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
       const uint32_t q = 8u * i + ql;
-      const T x = FO::load(wout + 16u * (8u * q + (u ^ ((q >> 1) & 7u))));
+      const T x = FO::load(w + 16u * (8u * q + (u ^ ((q >> 1) & 7u))));
       if (u < cnt && ((livemask >> q) & 1ull)) FO::store(wm.el(r0w + q, pos + u), x);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
-  const uint32_t nch = (total + kFwChunk - 1u) / kFwChunk;
-  stage(nch - 1u);  // in flight under the Lagrange weights
+  const uint32_t nch = (gp_len + kFwChunk - 1u) / kFwChunk;
+  stage(nch - 1u);  // in flight under the prefix products
 
   const T tm = FO::to_mont(FO::load(tq.at(rr)));
+  const T rm = FO::to_mont(FO::load(jr.at(rr)));
   T tmm = tm;
   for (uint32_t i = 0; i < logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
   const bool tbad = FO::eq(tmm, one);
 
-  // Lagrange weights: prefix products P_k = d_0 ... d_k, P_(k-1) parked in scratch entry k
+  // ---- forward: P_k = d_0 ... d_k (k <= C; P_(8b) parked for block b) beside RP[j] = r^(j+1) ----
   T P = FO::sub(tm, one);  // d_0 (alpha^0 = 1)
-  for (uint32_t k = 1; k <= C; ++k) {
-    FO::store(S(k), P);
-    P = FO::mul(P, FO::sub(tm, ld_tw<FO>(cfg, k)));
-  }
-  T inv = FO::mul(inv_mont128(P), FO::sub(tmm, one));  // (t^m - 1) / (d_0 ... d_C)
-  T lsum = FO::zero();
-  for (uint32_t hi = C + 1u; hi > 1u;) {  // blocks of 8, k = hi - 1 down to lo
-    const uint32_t nb = hi - 1u >= kFwChunk ? kFwChunk : hi - 1u;
-    const uint32_t lo = hi - nb;
-    T pb[kFwChunk];
-#pragma unroll
-    for (uint32_t u = 0; u < kFwChunk; ++u)
-      if (u < nb) pb[u] = FO::load(S(lo + u));
-#if FLPW_M3_BACK
-    // L_k = inv_k (P_(k-1) alpha^k/m): the chain step {inv pt_k, inv d_k} and the next entry's
-    // P_(k-2) alpha^(k-1)/m issue as one hazard-free triple
-    T ptw = one;
-#pragma unroll
-    for (int u = kFwChunk - 1; u >= 0; --u) {
-      if ((uint32_t)u < nb) {
-        const uint32_t k = lo + (uint32_t)u;
-        if ((uint32_t)u + 1u == nb) ptw = FO::mul(pb[u], ld_tw<FO>(cfg, 2u * m + 1u + k));
-        const T d = FO::sub(tm, ld_tw<FO>(cfg, k));
-        const T pn = u > 0 ? pb[u > 0 ? u - 1 : 0] : one;
-        const T tn = u > 0 ? ld_tw<FO>(cfg, 2u * m + k) : one;
-        T lk, ninv, nptw;
-        mul3<FO>(inv, ptw, inv, d, pn, tn, lk, ninv, nptw);
-        pb[u] = lk;
-        inv = ninv;
-        ptw = nptw;
-        FO::store(S(k), lk);
-        lsum = FO::add(lsum, lk);
-      }
-    }
-#else
-#pragma unroll
-    for (int u = kFwChunk - 1; u >= 0; --u) {
-      if ((uint32_t)u < nb) {
-        const uint32_t k = lo + (uint32_t)u;
-        pb[u] = FO::mul(FO::mul(inv, pb[u]), ld_tw<FO>(cfg, 2u * m + 1u + k));  // L_k
-        inv = FO::mul(inv, FO::sub(tm, ld_tw<FO>(cfg, k)));
-        FO::store(S(k), pb[u]);
-        lsum = FO::add(lsum, pb[u]);
-      }
-    }
-#endif
-    emit(C + lo - 1u, pb, nb);  // LM[lo .. lo + nb)
-    hi = lo;
-  }
-  const T l0 = FO::mul(inv, ld_tw<FO>(cfg, 2u * m + 1u));  // k = 0
-  const T half_l = FO::mul(lsum, FO::half());
-
-  // RP[j] = r^(j+1) (Montgomery), then rc = r^c
-  const T rm = FO::to_mont(FO::load(jr.at(rr)));
   T rp = one;
-  for (uint32_t j0 = 0; j0 < c; j0 += kFwChunk) {
-    T vb[kFwChunk];
-#pragma unroll
-    for (uint32_t u = 0; u < kFwChunk; ++u) {
-      if (j0 + u < c) {
-        rp = FO::mul(rp, rm);
-        vb[u] = rp;
-      }
+  const uint32_t steps = C > c ? C : c;
+  for (uint32_t k = 1; k <= steps; ++k) {
+    if (k <= C && ((k - 1u) & 7u) == 0u) FO::store(S((k - 1u) >> 3), P);
+    const T d = FO::sub(tm, ld_tw<FO>(cfg, k <= C ? k : 1u));
+    T nP, nrp, idle;
+    mul3<FO>(P, d, rp, rm, one, one, nP, nrp, idle);
+    if (k <= C) P = nP;
+    if (k <= c) {
+      rp = nrp;
+      const uint32_t u = (k - 1u) & 7u;
+      put(wout, u, rp);
+      if (u == 7u || k == c) flush(wout, W.rp((k - 1u) & ~7u), u + 1u);
     }
-    emit(2 * C + j0, vb, min(kFwChunk, c - j0));
   }
-  // MM[k] = LM[k] rc^(k-1)
-  T q = one;
-  T smm = FO::zero();
-  for (uint32_t k0 = 1; k0 <= C; k0 += kFwChunk) {
-    T vb[kFwChunk];
-#pragma unroll
-    for (uint32_t u = 0; u < kFwChunk; ++u)
-      if (k0 + u <= C) vb[u] = FO::load(S(k0 + u));
-#pragma unroll
-    for (uint32_t u = 0; u < kFwChunk; ++u) {
-      if (k0 + u <= C) {
-        vb[u] = FO::mul(vb[u], q);
-        smm = FO::add(smm, vb[u]);
-        q = FO::mul(q, rp);
-      }
-    }
-    emit(k0 - 1u, vb, min(kFwChunk, C + 1u - k0));
-  }
+  const T rc = rp;  // r^c
 
-  // proof share, last window first: gadget-poly coefficients (Horner needs d descending) and the
-  // wire seeds:  B0[j] = L0 s_2j,  B1[j] = L0 s_2j+1 - (1/2) sum_{k>=1} L_k
-  T pt = FO::zero();
-#if FLPW_M3_HORNER
+  // ---- p(t) and the gadget-output sum over the gadget coefficients, last window first ----
   // p(t) = A0(t^3) + t A1(t^3) + t^2 A2(t^3): three Horner chains in t^3 advanced as one triple per
   // group of coefficients (3g+2, 3g+1, 3g); c2/c1 park the group's first two
   const T t3 = FO::mul(FO::mul(tm, tm), tm);
   T A0 = FO::zero(), A1 = FO::zero(), A2 = FO::zero(), c2 = FO::zero(), c1 = FO::zero();
-#endif
   Wide gw;
   wide_zero(gw);
+  const uint8_t* myrow = win + 128u * lane;
   for (int ch = (int)nch - 1; ch >= 0; --ch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     T xb[kFwChunk];
@@ -1439,14 +1229,13 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       stage((uint32_t)ch - 1u);
     }
-    const uint32_t e0 = kFwChunk * (uint32_t)ch;  // even: a window holds whole seed pairs
+    const uint32_t e0 = kFwChunk * (uint32_t)ch;
 #pragma unroll
     for (int u = kFwChunk - 1; u >= 0; --u) {
-      const uint32_t e = e0 + (uint32_t)u;
-      if (e >= total || e < arity) continue;  // wave-uniform
+      const uint32_t e = e0 + (uint32_t)u;  // coefficient index (wave-uniform)
+      if (e >= gp_len) continue;
       bad |= !FO::is_canonical(xb[u]);
-#if FLPW_M3_HORNER
-      const uint32_t g3 = (e - arity) % 3u;  // wave-uniform
+      const uint32_t g3 = e % 3u;
       if (g3 == 2u) {
         c2 = xb[u];
       } else if (g3 == 1u) {
@@ -1458,58 +1247,79 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
         A1 = FO::add(n1, c1);
         A0 = FO::add(n0, xb[u]);
       }
-#else
-      pt = FO::add(FO::mul(pt, tm), xb[u]);
-#endif
-      wide_mac(gw, ld_tw<FO>(cfg, m + 1u + ((e - arity) & (m - 1u))), xb[u]);
-    }
-    if (e0 < arity) {  // wave-uniform
-      const uint32_t np = min(kFwChunk, arity - e0) / 2u;  // seed pairs in this window
-#if FLPW_M3_SEEDS
-      T lx[kFwChunk];  // L0 s_e for the window's seeds, three products at a time
-#pragma unroll
-      for (uint32_t u = 0; u < kFwChunk; u += 3) {
-        if (u < 2u * np) {
-          const T x1 = u + 1 < kFwChunk ? xb[u + 1 < kFwChunk ? u + 1 : 0] : one;
-          const T x2 = u + 2 < kFwChunk ? xb[u + 2 < kFwChunk ? u + 2 : 0] : one;
-          T r0, r1, r2;
-          mul3<FO>(l0, xb[u], l0, x1, l0, x2, r0, r1, r2);
-          lx[u] = r0;
-          if (u + 1 < kFwChunk) lx[u + 1 < kFwChunk ? u + 1 : 0] = r1;
-          if (u + 2 < kFwChunk) lx[u + 2 < kFwChunk ? u + 2 : 0] = r2;
-        }
-      }
-#endif
-      T bv[kFwChunk / 2];
-#pragma unroll
-      for (uint32_t h = 0; h < 2; ++h) {
-#pragma unroll
-        for (uint32_t u = 0; u < kFwChunk / 2; ++u) {
-          if (u < np) {
-            const T x = xb[2 * u + h];
-            bad |= !FO::is_canonical(x);
-#if FLPW_M3_SEEDS
-            (void)x;
-            bv[u] = h ? FO::sub(lx[2 * u + h], half_l) : lx[2 * u + h];
-#else
-            bv[u] = h ? FO::sub(FO::mul(l0, x), half_l) : FO::mul(l0, x);
-#endif
-          }
-        }
-        emit(2 * C + (1u + h) * c + e0 / 2u, bv, np);
-      }
+      wide_mac(gw, ld_tw<FO>(cfg, m + 1u + (e & (m - 1u))), xb[u]);
     }
   }
-#if FLPW_M3_HORNER
-  pt = FO::add(FO::mul(FO::add(FO::mul(A2, tm), A1), tm), A0);
-#endif
+  const T pt = FO::add(FO::mul(FO::add(FO::mul(A2, tm), A1), tm), A0);
   const T gsum = wide_reduce(gw);
+
+  // ---- one inversion for 1/(d_0 ... d_C) and 1/r^c; q = (r^c)^(C-1) for the descending MM ----
+  const bool rz = FO::is_zero(rc);  // r = 0: MM[1] = L_1, every other MM[k] = 0
+  T q = one;
+  {
+    T b = rc;
+    for (uint32_t e = C - 1u; e != 0u; e >>= 1) {
+      T nq, nb, idle;
+      mul3<FO>(q, b, b, b, one, one, nq, nb, idle);
+      if (e & 1u) q = nq;
+      b = nb;
+    }
+  }
+  const T iv = inv_mont128(rz ? P : FO::mul(P, rc));
+  T ivP, ivrc, idle0;
+  mul3<FO>(iv, P, iv, rc, one, one, ivP, ivrc, idle0);
+  const T rcinv = rz ? FO::zero() : ivP;
+  T inv = FO::mul(rz ? iv : ivrc, FO::sub(tmm, one));  // (t^m - 1) / (d_0 ... d_C)
+
+  // ---- backward, k = C .. 1 in blocks of 8: L_k = inv P_(k-1) alpha^k/m, inv <- inv d_k,
+  //      MM_k = L_k (r^c)^(k-1) (q <- q / r^c).  LM leaves through wout, MM through win. ----
+  T lsum = FO::zero(), smm = FO::zero();
+  for (int blk = (int)((C - 1u) >> 3); blk >= 0; --blk) {
+    const uint32_t lo = 8u * (uint32_t)blk + 1u;
+    const uint32_t nb = C - lo + 1u < kFwChunk ? C - lo + 1u : kFwChunk;
+    T pb[kFwChunk];
+    pb[0] = FO::load(S((uint32_t)blk));  // P_(lo - 1)
+#pragma unroll
+    for (uint32_t u = 1; u < kFwChunk; ++u)
+      if (u < nb) pb[u] = FO::mul(pb[u - 1], FO::sub(tm, ld_tw<FO>(cfg, lo + u - 1u)));
+    T ptw = one;
+#pragma unroll
+    for (int u = kFwChunk - 1; u >= 0; --u) {
+      if ((uint32_t)u < nb) {
+        const uint32_t k = lo + (uint32_t)u;
+        if ((uint32_t)u + 1u == nb) ptw = FO::mul(pb[u], ld_tw<FO>(cfg, 2u * m + 1u + k));
+        const T d = FO::sub(tm, ld_tw<FO>(cfg, k));
+        const T pn = u > 0 ? pb[u > 0 ? u - 1 : 0] : one;
+        const T tn = u > 0 ? ld_tw<FO>(cfg, 2u * m + k) : one;
+        T lk, ninv, nptw;
+        // the chain step {inv pt_k, inv d_k} and the next entry's P_(k-2) alpha^(k-1)/m
+        mul3<FO>(inv, ptw, inv, d, pn, tn, lk, ninv, nptw);
+        inv = ninv;
+        ptw = nptw;
+        T mm, nq, idle;
+        mul3<FO>(lk, q, q, rcinv, one, one, mm, nq, idle);
+        if (rz) mm = k == 1u ? lk : FO::zero();
+        q = nq;
+        put(wout, (uint32_t)u, lk);
+        put(win, (uint32_t)u, mm);
+        lsum = FO::add(lsum, lk);
+        smm = FO::add(smm, mm);
+      }
+    }
+    flush(wout, W.lm(lo - 1u), nb);
+    flush(win, W.mm(lo - 1u), nb);
+  }
+  const T l0 = FO::mul(inv, ld_tw<FO>(cfg, 2u * m + 1u));  // k = 0
+  const T hl = FO::mul(lsum, FO::half());
+
   if (!live) return;
-  FO::store(wm.el(rr, 2 * C + 3 * c), gsum);
-  FO::store(wm.el(rr, 2 * C + 3 * c + 1), smm);
-  FO::store(wm.el(rr, 2 * C + 3 * c + 2), lsum);
+  FO::store(wm.el(rr, W.l0()), l0);
+  FO::store(wm.el(rr, W.hl()), hl);
+  FO::store(wm.el(rr, W.gsum()), gsum);
+  FO::store(wm.el(rr, W.smm()), smm);
+  FO::store(wm.el(rr, W.slm()), lsum);
   uint8_t* outp = out_prep.at(rr);
-  if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: k_flp_wires)
+  if (cfg.kind != KIND_HISTOGRAM) FO::store(outp, gsum);  // v (Histogram: the wire pass)
   FO::store(outp + (size_t)(1 + arity) * 16, pt);
   const uint8_t* pp = part.at(rr);
   uint8_t* dst = outp + (size_t)cfg.verifier_len * 16;
@@ -1527,9 +1337,11 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
 // ------------------------------------------------------------------------------------------------
 template <class FO>
 __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims dims, CRows meas,
-                                                   WMat wm, CRows jr, Rows out_prep,
+                                                   CRows proof, WMat wm, CRows jr, Rows out_prep,
                                                    uint8_t* status) {
   using T = typename FO::T;
+  static_assert(FO::ES == 16, "ParallelSum types are Field128");
+  const WRow W(cfg);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t r = blockIdx.x;
   if (r >= n) return;
@@ -1617,11 +1429,11 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
       a = FO::add(a, PA[h * c + j]);
       b = FO::add(b, PB[h * c + j]);
     }
-    const T rp = FO::load(wm.el(r, 2 * C + j));  // Montgomery
-    const T w0 = FO::add(FO::load(wm.el(r, 2 * C + c + j)), FO::mul(rp, a));
-    const T w1 = FO::add(FO::load(wm.el(r, 2 * C + 2 * c + j)), b);
-    FO::store(outp + (size_t)(1 + 2 * j) * ES, w0);
-    FO::store(outp + (size_t)(2 + 2 * j) * ES, w1);
+    T b0, b1;
+    wire_seed_terms(wm, W, r, proof.at(r), j, b0, b1, bad);
+    const T rp = FO::load(wm.el(r, W.rp(j)));  // Montgomery
+    FO::store(outp + (size_t)(1 + 2 * j) * ES, FO::add(b0, FO::mul(rp, a)));
+    FO::store(outp + (size_t)(2 + 2 * j) * ES, FO::add(b1, b));
   }
   if (bad) atomicOr(flag, 1u);
   if (cfg.kind == KIND_HISTOGRAM) xsum = block_sum<FO>(xsum, RED, tid, nthr);
@@ -1629,7 +1441,7 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
   if (tid == 0) {
     if (cfg.kind == KIND_HISTOGRAM) {
       // v = jr[1] * range + jr[1]^2 * (sum x - 1/2)
-      const T gsum = FO::load(wm.el(r, 2 * C + 3 * c));
+      const T gsum = FO::load(wm.el(r, W.gsum()));
       const T r1m = FO::to_mont(FO::load(jr.at(r) + ES));
       const T sc = FO::sub(xsum, FO::half());
       FO::store(outp, FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc)));
@@ -1648,9 +1460,10 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
 // partials, three barriers, a one-thread tail) on each Histogram(256) report.
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_flp_wires_cols(Cfg cfg, uint32_t n, uint32_t lg, CRows meas,
-                                                        WMat wm, CRows jr, Rows out_prep,
-                                                        uint8_t* status) {
+                                                        CRows proof, WMat wm, CRows jr,
+                                                        Rows out_prep, uint8_t* status) {
   using FO = Field128Ops;
+  const WRow W(cfg);
   using T = F128;
   constexpr size_t ES = 16;
   const uint32_t G = 1u << lg;
@@ -1681,10 +1494,11 @@ __global__ void __launch_bounds__(256) k_flp_wires_cols(Cfg cfg, uint32_t n, uin
   const T a = wide_reduce(wa), b = wide_reduce(wb);
   uint8_t* outp = out_prep.at(rr);
   if (col) {
-    const T rp = FO::load(wm.el(rr, 2 * C + j));  // Montgomery
-    FO::store(outp + (size_t)(1 + 2 * j) * ES,
-              FO::add(FO::load(wm.el(rr, 2 * C + c + j)), FO::mul(rp, a)));
-    FO::store(outp + (size_t)(2 + 2 * j) * ES, FO::add(FO::load(wm.el(rr, 2 * C + 2 * c + j)), b));
+    T b0, b1;
+    wire_seed_terms(wm, W, rr, proof.at(rr), j, b0, b1, bad);
+    const T rp = FO::load(wm.el(rr, W.rp(j)));  // Montgomery
+    FO::store(outp + (size_t)(1 + 2 * j) * ES, FO::add(b0, FO::mul(rp, a)));
+    FO::store(outp + (size_t)(2 + 2 * j) * ES, FO::add(b1, b));
   }
   if (cfg.kind == KIND_HISTOGRAM) {
     for (uint32_t sft = G >> 1; sft > 0; sft >>= 1) {
@@ -1697,7 +1511,7 @@ __global__ void __launch_bounds__(256) k_flp_wires_cols(Cfg cfg, uint32_t n, uin
   if (!live || j != 0u) return;
   if (cfg.kind == KIND_HISTOGRAM) {
     // v = jr[1] * range + jr[1]^2 * (sum x - 1/2)
-    const T gsum = FO::load(wm.el(rr, 2 * C + 3 * c));
+    const T gsum = FO::load(wm.el(rr, W.gsum()));
     const T r1m = FO::to_mont(FO::load(jr.at(rr) + ES));
     const T sc = FO::sub(xsum, FO::half());
     FO::store(outp, FO::add(FO::mul(r1m, gsum), FO::mul(FO::mul(r1m, r1m), sc)));

@@ -65,8 +65,8 @@ __host__ __device__ inline size_t wires_mfma_e_bytes(uint32_t calls) {
   return (size_t)(2 * ((calls + 1) / 2)) * 2 * kWmEDwords * 4;
 }
 
-__global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRows meas, WMat wm,
-                                                         CRows jr, Rows out_prep, uint8_t* status) {
+__global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRows meas, CRows proof,
+                                                         WMat wm, Rows out_prep, uint8_t* status) {
   using FO = Field128Ops;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
   const uint32_t wv = wave;             // this wave's first tile
   const uint32_t pt = tid, npt = blockDim.x;  // weight conversion
   const uint32_t C = cfg.calls, c = cfg.chunk, KQ = (C + 1) / 2;
+  const WRow W(cfg);
   uint32_t* E = reinterpret_cast<uint32_t*>(smem);
   uint32_t* flag = reinterpret_cast<uint32_t*>(smem + wires_mfma_e_bytes(C));
   if (tid == 0) *flag = 0u;
@@ -113,7 +114,7 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
 #pragma unroll
     for (uint32_t w = 0; w < 2; ++w) {
       F128 x = FO::zero();
-      if (k < C) x = FO::load(wm.el(r, w * C + k));
+      if (k < C) x = FO::load(wm.el(r, w ? W.lm(k) : W.mm(k)));
       // y = x + K128; digits d_b = y_b - 128 (b < 16), d_16 = carry out
       uint32_t D[4], cy = 0u;
 #pragma unroll
@@ -210,7 +211,7 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
     // + K128 * W', W' = (sum_k w_k mod p) + calls p >= sum_k w_k (the integer), so the total stays
     // >= 0 and == sum_k w_k x_k (mod p); the sums come from k_flp_weights (SMM, SLM)
     {
-      const F128 wsum = FO::load(wm.el(r, 2 * C + 3 * c + 1 + h));
+      const F128 wsum = FO::load(wm.el(r, h ? W.slm() : W.smm()));
       uint32_t Wd[6];
       {
         const int64_t CC = (int64_t)C;
@@ -253,12 +254,17 @@ __global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRo
     wd.hi[6] = S[8];
     const F128 v = wide_reduce(wd);
     if (colok) {
+      // wire 2j + h = L0 s_(2j+h) (- HL for h = 1) + (RP[j] a_j | b_j)
       uint8_t* outp = out_prep.at(r);
+      const F128 l0 = FO::load(wm.el(r, W.l0()));
+      const F128 sd = FO::load(proof.at(r) + (size_t)(2 * j + h) * 16);
+      bad |= !FO::is_canonical(sd);
       if (h == 0) {
-        const F128 rp = FO::load(wm.el(r, 2 * C + j));  // Montgomery
-        FO::store(outp + (size_t)(1 + 2 * j) * 16, FO::add(FO::load(wm.el(r, 2 * C + c + j)), FO::mul(rp, v)));
+        const F128 rp = FO::load(wm.el(r, W.rp(j)));  // Montgomery
+        FO::store(outp + (size_t)(1 + 2 * j) * 16, FO::add(FO::mul(l0, sd), FO::mul(rp, v)));
       } else {
-        FO::store(outp + (size_t)(2 + 2 * j) * 16, FO::add(FO::load(wm.el(r, 2 * C + 2 * c + j)), v));
+        FO::store(outp + (size_t)(2 + 2 * j) * 16,
+                  FO::add(FO::sub(FO::mul(l0, sd), FO::load(wm.el(r, W.hl()))), v));
       }
     }
   }

@@ -313,7 +313,7 @@ class Prio3Gpu:
 
     def set_option(self, name: str, value: int):
         """Engine option of this context (prio3gpu_ctx_set_option: "speculate", "wires_mfma",
-        "wires_cols", "sum_split", "fused_helper", "jr_ring", "spread", "expand_lds", "jr_lds",
+        "wires_cols", "fused_helper", "jr_ring", "spread", "expand_lds", "jr_lds",
         "exact_squeeze")."""
         check(lib().prio3gpu_ctx_set_option(self._ctx, name.encode(), int(value)),
               f"ctx_set_option({name})")
@@ -354,6 +354,13 @@ class Prio3Gpu:
         n = _nbytes(status)
         check(lib().prio3gpu_prepare_init_query(self._ctx, state._h, n, _ptr(out_prep_shares),
                                                 _ptr(status)), "prepare_init_query")
+
+    def prepare_init_weights(self, state: PrepareState, status):
+        """Optional step between the XOF and query phases: the first (latency-bound) half of a
+        ParallelSum FLP query (k_flp_weights); a no-op for the other types."""
+        n = _nbytes(status)
+        check(lib().prio3gpu_prepare_init_weights(self._ctx, state._h, n, _ptr(status)),
+              "prepare_init_weights")
 
     def new_state(self, agg_id: int, capacity: int) -> PrepareState:
         return PrepareState(self, agg_id, capacity)

@@ -183,6 +183,8 @@ extern "C" {
     pub fn prio3gpu_prepare_init_xof(ctx: *mut prio3gpu_ctx, st: *mut prio3gpu_state, n: usize,
                                      nonces: *const u8, public_shares: *const u8,
                                      input_shares: *const u8, status: *mut u8) -> c_int;
+    pub fn prio3gpu_prepare_init_weights(ctx: *mut prio3gpu_ctx, st: *mut prio3gpu_state, n: usize,
+                                         status: *mut u8) -> c_int;
     pub fn prio3gpu_prepare_init_query(ctx: *mut prio3gpu_ctx, st: *mut prio3gpu_state,
                                        n: usize, out_prep_shares: *mut u8,
                                        status: *mut u8) -> c_int;

@@ -256,3 +256,26 @@ def test_rccl_flushes_of_two_async_contexts_on_one_comm():
     for loc in locals_:
         assert loc.read(0)[1] == 0
     comm.close()
+
+
+@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "sumvec_8_1000", "sum8", "fp16_3"])
+def test_three_phase_prepare_init_matches_oracle(name):
+    """prepare_init as XOF phase -> weights phase (prio3gpu_prepare_init_weights: ParallelSum
+    types' k_flp_weights; a no-op otherwise) -> query phase, for both aggregators: the oracle's
+    prep shares; the weights phase twice is harmless, and the query phase alone still works."""
+    from tests.test_gpu_parity import batch, gpu_vdaf
+    b = batch(name)  # the transcript tests' cached oracle batch
+    v = gpu_vdaf(b)
+    s = v.sizes
+    for agg_id, inp, want in ((0, b.leader_in, b.leader_prep), (1, b.helper_in, b.helper_prep)):
+        for weights in (0, 1, 2):
+            st = v.new_state(agg_id, b.n)
+            status = np.zeros(b.n, np.uint8)
+            v.prepare_init_xof(st, b.nonces, b.public if s.public_share else None, inp, status)
+            for _ in range(weights):
+                v.prepare_init_weights(st, status)
+            out = np.zeros((b.n, s.prep_share), np.uint8)
+            v.prepare_init_query(st, out, status)
+            assert (status == 0).all()
+            np.testing.assert_array_equal(out, want)
+            st.close()
