@@ -50,7 +50,7 @@ VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 # Measured register-only Keccak-f[1600] ceiling of one MI355X (tools/mb_keccak_occ.hip,
 # profiles/microbench_keccak_mem_r01.log: 10.3-10.8 G permutations/s at 2-6 waves/SIMD)
 KECCAK_CEILING = 10.8e9
-PMC_ROUND = "r03"
+PMC_ROUND = "r04"
 
 
 def cpu_threads(requested=0):
@@ -108,15 +108,15 @@ def load_pmc(config):
 
 def flp_wires_bytes_per_report(s, mfma=False):
     """Algorithmic HBM bytes of the FLP wire pass per report (ParallelSum types): the measurement
-    share once, the weight-row entries it reads -- MM[calls] | LM[calls] | RP[c] | B0[c] | B1[c],
-    plus gsum (k_flp_wires) or SMM, SLM (k_flp_wires_mfma) -- and the 2c wire values written into
-    the prep share."""
+    share once, the weight-row entries it reads -- MM[calls] | LM[calls] | RP[c] | L0 | HL, plus
+    SMM, SLM (k_flp_wires_mfma's offset correction) -- the 2c wire seeds of the proof share, and
+    the 2c wire values written into the prep share."""
     es = s.field_size
     arity = s.verifier_len - 2
     c = arity // 2
     calls = -(-s.meas_len // c)
-    w_len = 2 * calls + 3 * c + (2 if mfma else 1)
-    return (s.meas_len + w_len + arity) * es
+    w_len = 2 * calls + c + (4 if mfma else 2)
+    return (s.meas_len + w_len + 2 * arity) * es
 
 
 def flp_mults_per_report(sizes, kind):

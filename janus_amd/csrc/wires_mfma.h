@@ -65,7 +65,8 @@ __host__ __device__ inline size_t wires_mfma_e_bytes(uint32_t calls) {
   return (size_t)(2 * ((calls + 1) / 2)) * 2 * kWmEDwords * 4;
 }
 
-__global__ void __launch_bounds__(256) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRows meas, CRows proof,
+// 4 waves per SIMD (<= 128 VGPRs): the pass hides HBM latency with occupancy
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_flp_wires_mfma(Cfg cfg, uint32_t n, CRows meas, CRows proof,
                                                          WMat wm, Rows out_prep, uint8_t* status) {
   using FO = Field128Ops;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
