@@ -25,6 +25,7 @@
 #include "keccak.h"
 #include "wide.h"
 #include "mont3.h"
+#include "mont_fma.h"
 
 namespace p3g {
 
@@ -861,6 +862,80 @@ DEVI typename FO::T inv_mont(const typename FO::T& x) {
   else return inv_mont64(x);
 }
 
+// Sum's FLP query when calls = m/2 (power-of-two bits) and r^m != 1, Field128, one lane per report:
+// the same field values as the generic loop below, from fewer products:
+//   * the gadget-output sum  v = sum_i F_i G(y_i),  y_i = r alpha^i,  G(y) = y (y^calls - 1)/(y - 1):
+//     y_i^calls = r^calls (-1)^i =: s_i, so with c_par = s_i - 1 (two constants) and
+//     y/(y - 1) = 1 + 1/(y - 1):   v = sum_par c_par (sum_(i = par) F_i + sum_(i = par) F_i/(y_i - 1))
+//     -- two running fractions N/D (even and odd i) updated as N e + F D (ONE fused product),
+//     D e, plus a plain sum of F;
+//   * the wire  sum_(k=0..calls) alpha^k x_k/(t - alpha^k) = t sum_k x_k/(t - alpha^k) - sum_k x_k
+//     (alpha^k/(t - alpha^k) = t/(t - alpha^k) - 1): the running fraction N d + x D (fused), D d, no
+//     alpha^k x product; k = 0 (x_0 = the proof seed) is iteration i = 0;
+//   * p(t) = sum_i (c_i + t^m c_(i+m)) t^i as ONE fused product t pt + t^m c_(i+m) per i;
+//   * the three denominators share one inversion.
+// Products issue as interleaved fused / single Montgomery streams (mont_fma.h): per iteration
+// 2 fused + 2 single (non-wire i) or 3 fused + 3 single (wire i) against 8 / 12 products before.
+// Domains: values marked M are Montgomery form (x R), the rest plain; mont(M, plain) is plain.
+DEVI void sum_query_half(const Cfg& cfg, const F128& tm, const F128& tmm, const F128& rm,
+                         const F128& rc, const uint8_t* gp, const uint8_t* xr, const F128& s0,
+                         bool& bad, F128& pt_out, F128& w0_out, F128& v_out) {
+  using FO = Field128Ops;
+  using T = F128;
+  const uint32_t m = cfg.m, calls = cfg.calls, gp_len = cfg.gp_len;
+  const T one = FO::one_mont();
+  T pt = FO::zero();                      // Horner, plain
+  T N[2] = {FO::zero(), FO::zero()};      // v fractions (even, odd i), plain
+  T D[2] = {one, one};                    // their denominators, M
+  T S[2] = {FO::zero(), FO::zero()};      // sums of F by parity, plain
+  T Nw = FO::zero(), Dw = one, X = FO::zero();  // wire fraction (plain / M) and sum x (plain)
+  T y = FO::mul(rm, ld_tw<FO>(cfg, m - 1u));     // y_(m-1), M
+  for (uint32_t i = m - 1;; --i) {
+    const T ci = FO::load(gp + (size_t)i * 16);
+    const T ch = i + m < gp_len ? FO::load(gp + (size_t)(i + m) * 16) : FO::zero();
+    bad |= !FO::is_canonical(ci) || !FO::is_canonical(ch);
+    const T f = FO::add(ci, ch);
+    const T e = FO::sub(y, one);                       // M(y - 1)
+    const uint32_t par = i & 1u;                       // loop-uniform
+    S[par] = FO::add(S[par], f);
+    const T twn = ld_tw<FO>(cfg, i ? i - 1u : 0u);      // alpha^(i-1): the next y
+    T PQ, VN, yn, VD;
+    if (i <= calls) {  // wire term k = i (x_0 = the proof seed)
+      const T x = i ? FO::load(xr + (size_t)(i - 1) * 16) : s0;
+      if (i) bad |= !FO::is_canonical(x);
+      X = FO::add(X, x);
+      const T d = FO::sub(tm, ld_tw<FO>(cfg, i));       // M(t - alpha^i)
+      mont_fma2_mul1(tm, pt, tmm, ch, PQ, N[par], e, f, D[par], VN, rm, twn, yn);
+      T NW, DW;
+      mont_fma1_mul2(Nw, d, x, Dw, NW, Dw, d, DW, D[par], e, VD);
+      Nw = NW;
+      Dw = DW;
+    } else {
+      mont_fma2_mul2(tm, pt, tmm, ch, PQ, N[par], e, f, D[par], VN, rm, twn, yn, D[par], e, VD);
+    }
+    pt = FO::add(PQ, ci);
+    N[par] = VN;
+    D[par] = VD;
+    y = yn;
+    if (i == 0) break;
+  }
+  // one inversion for Dw, D0, D1
+  T t1, t2, t3;
+  mul3<FO>(D[0], D[1], Dw, D[1], Dw, D[0], t1, t2, t3);  // M(D0 D1), M(Dw D1), M(Dw D0)
+  const T inv = inv_mont128(FO::mul(Dw, t1));            // M(1 / (Dw D0 D1))
+  T iw, i0, i1;
+  mul3<FO>(inv, t1, inv, t2, inv, t3, iw, i0, i1);       // M(1/Dw), M(1/D0), M(1/D1)
+  T qw, q0, q1;
+  mul3<FO>(Nw, iw, N[0], i0, N[1], i1, qw, q0, q1);      // plain fractions
+  const T cm = FO::mul(FO::sub(tmm, one), ld_tw<FO>(cfg, m));  // M((t^m - 1)/m)
+  const T c0 = FO::sub(rc, one), c1 = FO::sub(FO::sub(FO::zero(), rc), one);  // M(s_par - 1)
+  T tq, v0, v1;
+  mul3<FO>(tm, qw, c0, FO::add(S[0], q0), c1, FO::add(S[1], q1), tq, v0, v1);
+  w0_out = FO::mul(cm, FO::sub(tq, X));
+  v_out = FO::add(v0, v1);
+  pt_out = pt;
+}
+
 #ifndef FLPQ_WAVES
 #define FLPQ_WAVES
 #endif
@@ -954,7 +1029,27 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
       vn = FO::add(FO::mul(vn, e), FO::mul(b, vd));
       vd = FO::mul(vd, e);
     };
-    if (!r_root && FLPQ_MUL3) {
+    bool done = false;
+    if constexpr (FO::ES == 16) {
+      if (!r_root && 2u * calls == m && arity == 1) {
+        T w0, v;
+        sum_query_half(cfg, tm, tmm, rm, rc, gp, xr, s0, bad, pt, w0, v);
+        uint8_t* outp = out_prep.at(r);
+        FO::store(outp, v);
+        FO::store(outp + ES, w0);
+        FO::store(outp + (size_t)(1 + arity) * ES, pt);
+        const uint8_t* pp = part.at(r);
+        uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
+        st64(dst, ld64(pp));
+        st64(dst + 8, ld64(pp + 8));
+        if (bad) status[r] = ST_INVALID_MESSAGE;
+        else if (root) status[r] = ST_VDAF_PREP_ERROR;
+        done = true;
+      }
+    }
+    if (done) {
+      return;
+    } else if (!r_root && FLPQ_MUL3) {
       // the same three chains, every iteration's products issued as hazard-free triples
       // (mont_mul3, Field128).  b_i * vd is refactored as (y f) * ((yc - 1) vd) so the
       // 12 (13) products of a wire iteration form 4 triples (+1 single); when calls == m / 2

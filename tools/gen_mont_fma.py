@@ -1,0 +1,403 @@
+#!/usr/bin/env python3
+"""Generate janus_amd/csrc/mont_fma.h: Field128 Montgomery products and FUSED product sums
+    fma:  r = (a b + c d) 2^-128 mod p        mul:  r = a b 2^-128 mod p
+issued as three interleaved instruction streams (gfx950 inline asm), every program checked here by
+simulating the exact instruction list, including the register aliasing, and every carry read
+checked against gfx950's VALU carry hazard (a VALU that writes an SGPR carry / VCC needs two wait
+states before a VALU reads it): where the interleaving does not provide them, s_nop is emitted.
+
+Why fused: a Montgomery product is 16 v_mad_u64_u32 + ~74 carry / shift instructions, of which
+the two REDC steps and the final subtraction are ~2/3.  The fraction and Horner recurrences of
+the FLP query (N d + a D, t pt + t^m c) are sums of two products: accumulating both products'
+columns before ONE reduction saves ~30 % of their instructions (the sum is < 2 p^2 < 2^257, so
+the reduction takes nine input words and ends with up to two conditional subtractions).
+
+The operations of one function ("F" fused / "M" single) are independent and issue as one stream
+each, round-robin; their product phases go into the first asm statement (64-bit column
+accumulators, v_mad_u64_u32 writes pairs), their reductions into the second (32-bit halves: C++
+splits the pairs between the statements, register renaming only).
+
+  python3 tools/gen_mont_fma.py          # simulate + write janus_amd/csrc/mont_fma.h
+"""
+import os
+import random
+
+P = (1 << 128) - 28 * (1 << 64) + 1
+M32 = (1 << 32) - 1
+P2 = 0xFFFFFFE4
+R = 1 << 128
+
+
+# ---------------------------------------------------------------------------------------------
+# programs of one operation (register names local to the operation, prefix added later)
+# ---------------------------------------------------------------------------------------------
+def product(fused):
+    """Column sums of a b (+ c d): L0..L6 (64-bit), carries h0..h6 (32-bit; h_c sits at
+    2^(32 c + 64)).  Each mad's carry is read by the addc right after it (the interleave or the
+    emitter's s_nop gives the wait states)."""
+    ins = []
+    first = set()
+    pairs = [("a", "b")] + ([("c", "d")] if fused else [])
+    for (x, y) in pairs:
+        for c in range(7):
+            for i in range(4):
+                j = c - i
+                if not 0 <= j < 4:
+                    continue
+                if c not in first:
+                    first.add(c)
+                    ins.append(("mad", f"L{c}", "cd", f"{x}{i}", f"{y}{j}", 0))
+                else:
+                    ins.append(("mad", f"L{c}", "cy", f"{x}{i}", f"{y}{j}", f"L{c}"))
+                    ins.append(("addc", f"h{c}", "cd", f"h{c}", 0, "cy"))
+    return ins
+
+
+def product_inits():
+    return [f"h{c}" for c in range(7)]  # zero-initialised carry words
+
+
+def reduce_program(fused):
+    """T = sum_c L_c 2^(32c) + sum_c h_c 2^(32c+64) -> (T / 2^128) mod p, canonical, in r0..r3.
+    Inputs l0..l6 / g0..g6 (halves of L0..L6), h0..h6."""
+    ins = []
+    A = ins.append
+    A(("add_co", "l1", "k", "l1", "g0"))
+    for c in range(2, 7):
+        A(("addc", f"l{c}", "k", f"l{c}", f"g{c - 1}", "k"))
+    A(("addc", "g6", "k", "g6", 0, "k"))
+    A(("addc", "h6", "k", "h6", 0, "k"))
+    T = ["l0", "l1", "l2", "l3", "l4", "l5", "l6", "g6", "h6"]
+    A(("add_co", T[2], "k", T[2], "h0"))
+    for c in range(3, 8):
+        A(("addc", T[c], "k", T[c], f"h{c - 2}", "k"))
+    A(("addc", T[8], "k", T[8], 0, "k"))
+
+    def redc(X, n):
+        A(("sub_co", "m0", "k", 0, X[0]))
+        A(("subb", "m1", "k", 0, X[1], "k"))
+        A(("lsl", "a0", 5, "m0"))
+        A(("abit", "a1", "m1", "m0", 27))
+        A(("lsr", "a2", 27, "m1"))
+        A(("lsl", "b0", 2, "m0"))
+        A(("abit", "b1", "m1", "m0", 30))
+        A(("lsr", "b2", 30, "m1"))
+        A(("sub_co", "w0", "k2", "a0", "b0"))  # 28 m = 32 m - 4 m (96 bits)
+        A(("subb", "w1", "k2", "a1", "b1", "k2"))
+        A(("subb", "w2", "k2", "a2", "b2", "k2"))
+        Y = X[2:2 + n]
+        A(("addc", Y[0], "k", Y[0], 0, "k"))
+        A(("addc", Y[1], "k", Y[1], 0, "k"))
+        A(("addc", Y[2], "k", Y[2], "m0", "k"))
+        A(("addc", Y[3], "k", Y[3], "m1", "k"))
+        for i in range(4, n):
+            A(("addc", Y[i], "k", Y[i], 0, "k"))
+        A(("sub_co", Y[0], "k2", Y[0], "w0"))
+        A(("subb", Y[1], "k2", Y[1], "w1", "k2"))
+        A(("subb", Y[2], "k2", Y[2], "w2", "k2"))
+        for i in range(3, n):
+            A(("subb", Y[i], "k2", Y[i], 0, "k2"))
+        return Y
+
+    U = redc(T, 7)  # (T + m p) / 2^64 < 2^194: 7 words
+    V = redc(U, 5)  # < 3 p < 2^130: 5 words
+    # up to two conditional subtractions of p (one suffices for a single product: V < 2p)
+    for rnd in range(2 if fused else 1):
+        A(("sub_co", "m0", "k", V[0], 1))
+        A(("subb", "a0", "k", V[1], 0, "k"))
+        A(("subb", "a1", "k", V[2], "P2", "k"))
+        A(("subb", "a2", "k", V[3], -1, "k"))
+        A(("subb", "b0", "k", V[4], 0, "k"))  # k = borrow: V < p
+        dst = ["r0", "r1", "r2", "r3", None] if rnd == (1 if fused else 0) else V
+        A(("cnd", dst[0], "m0", V[0], "k"))
+        A(("cnd", dst[1], "a0", V[1], "k"))
+        A(("cnd", dst[2], "a1", V[2], "k"))
+        A(("cnd", dst[3], "a2", V[3], "k"))
+        if dst is V:
+            A(("cnd", V[4], "b0", V[4], "k"))
+    return ins
+
+
+# temporaries of the reduction in registers the normalisation has freed
+ALIAS = {"m0": "g0", "m1": "g1", "a0": "g2", "a1": "g3", "a2": "g4", "b0": "g5", "b1": "h1",
+         "b2": "h2", "w0": "h3", "w1": "h4", "w2": "h5"}
+
+
+# ---------------------------------------------------------------------------------------------
+# simulator (one lane)
+# ---------------------------------------------------------------------------------------------
+def val(st, x):
+    if isinstance(x, int):
+        return x & M32
+    if x == "P2":
+        return P2
+    return st[x]
+
+
+def simulate(prog, st):
+    for ins in prog:
+        op = ins[0]
+        if op == "mad":
+            _, d, c, s0, s1, s2 = ins
+            t = val(st, s0) * val(st, s1) + (0 if s2 == 0 else st[s2])
+            st[d] = t & ((1 << 64) - 1)
+            st[c] = t >> 64
+        elif op in ("add_co", "addc"):
+            d, c, s0, s1 = ins[1:5]
+            t = val(st, s0) + val(st, s1) + (st[ins[5]] if op == "addc" else 0)
+            st[d], st[c] = t & M32, t >> 32
+        elif op in ("sub_co", "subb"):
+            d, c, s0, s1 = ins[1:5]
+            t = val(st, s0) - val(st, s1) - (st[ins[5]] if op == "subb" else 0)
+            st[d], st[c] = t & M32, 1 if t < 0 else 0
+        elif op == "lsl":
+            st[ins[1]] = (val(st, ins[3]) << ins[2]) & M32
+        elif op == "lsr":
+            st[ins[1]] = val(st, ins[3]) >> ins[2]
+        elif op == "abit":
+            st[ins[1]] = (((val(st, ins[2]) << 32) | val(st, ins[3])) >> ins[4]) & M32
+        elif op == "cnd":
+            st[ins[1]] = val(st, ins[3]) if st[ins[4]] else val(st, ins[2])
+        elif op == "nop":
+            pass
+        else:
+            raise ValueError(op)
+
+
+def aliased(prog):
+    return [tuple(ALIAS.get(x, x) if isinstance(x, str) else x for x in ins) for ins in prog]
+
+
+def run_op(fused, a, b, c=0, d=0):
+    st = {}
+    for i in range(4):
+        st[f"a{i}"], st[f"b{i}"] = (a >> (32 * i)) & M32, (b >> (32 * i)) & M32
+        st[f"c{i}"], st[f"d{i}"] = (c >> (32 * i)) & M32, (d >> (32 * i)) & M32
+    for h in product_inits():
+        st[h] = 0
+    simulate(product(fused), st)
+    for k in range(7):
+        st[f"l{k}"], st[f"g{k}"] = st[f"L{k}"] & M32, st[f"L{k}"] >> 32
+    simulate(aliased(reduce_program(fused)), st)
+    return sum(st[f"r{i}"] << (32 * i) for i in range(4))
+
+
+def check(trials=20000):
+    rng = random.Random(7)
+    edge = [0, 1, 2, P - 1, P - 2, 1 << 64, 1 << 127, P // 2, (1 << 128) - 28 * (1 << 64)]
+    rinv = pow(R, -1, P)
+    pick = lambda t, k: rng.choice(edge) if t % k == 0 else rng.randrange(P)
+    for t in range(trials):
+        a, b, c, d = pick(t, 7), pick(t, 5), pick(t, 3), pick(t, 11)
+        assert run_op(False, a, b) == a * b * rinv % P, (a, b)
+        assert run_op(True, a, b, c, d) == (a * b + c * d) * rinv % P, (a, b, c, d)
+    for a, b in [(P - 1, P - 1), (P - 2, P - 1)]:  # the largest sums
+        assert run_op(True, a, b, a, b) == 2 * a * b * rinv % P
+    return trials
+
+
+# ---------------------------------------------------------------------------------------------
+# emitter: streams interleaved round-robin; s_nop wherever a carry would be read too early
+# ---------------------------------------------------------------------------------------------
+CARRY_OPS = {"mad": 2, "add_co": 2, "addc": 2, "sub_co": 2, "subb": 2}  # index of carry-out
+WAIT = 2  # wait states between a VALU carry write and a VALU carry read
+
+
+def interleave(streams):
+    """streams: lists of (ins, stream_id).  Round-robin; returns the issue order with ("nop", n)
+    entries so that every read of a carry register is >= WAIT + 1 slots after its write."""
+    out = []
+    last_write = {}  # register (stream-qualified) -> issue slot
+    pos = [0] * len(streams)
+    slot = 0
+    while any(p < len(s) for p, s in zip(pos, streams)):
+        for k, s in enumerate(streams):
+            if pos[k] >= len(s):
+                continue
+            ins, sid = s[pos[k]]
+            pos[k] += 1
+            reads = []
+            op = ins[0]
+            if op in ("addc", "subb"):
+                reads.append(ins[5])
+            elif op == "cnd":
+                reads.append(ins[4])
+            need = 0
+            for r in reads:
+                key = (sid, r)
+                if key in last_write:
+                    need = max(need, last_write[key] + WAIT + 1 - slot)
+            if need > 0:
+                out.append((("nop", need - 1), None))  # s_nop N waits N + 1 slots
+                slot += need
+            out.append((ins, sid))
+            if op in CARRY_OPS:
+                last_write[(sid, ins[CARRY_OPS[op]])] = slot
+            slot += 1
+    return out
+
+
+def gen_function(name, spec):
+    """spec: one string per stream of "F" (fused) / "M" (single) operations, e.g. ["F", "F", "MM"].
+    Signature: for every operation in stream order, (a, b[, c, d]) inputs then its output."""
+    ops = []  # (stream, op index in stream, fused, tag)
+    for s, st in enumerate(spec):
+        for q, kind in enumerate(st):
+            ops.append((s, q, kind == "F", f"{s}{q}"))
+    out = []
+    w = out.append
+    params = []
+    for s, q, fused, tag in ops:
+        params += [f"const F128& a{tag}", f"const F128& b{tag}"]
+        if fused:
+            params += [f"const F128& c{tag}", f"const F128& d{tag}"]
+        params.append(f"F128& r{tag}")
+    w(f"DEVI void {name}(" + ", ".join(params) + ") {")
+    # ---- products ----
+    ops_e, cons = [], []
+    idx = {}
+
+    def opnd(key, con, expr):
+        idx[key] = len(ops_e)
+        ops_e.append(expr)
+        cons.append(con)
+
+    for s, q, fused, tag in ops:
+        w(f"  uint64_t L{tag}[7];")
+        w(f"  uint32_t h{tag}[7] = {{0u, 0u, 0u, 0u, 0u, 0u, 0u}};")
+        w(f"  uint64_t cy{tag};")
+    w("  uint64_t cdump;")
+    for s, q, fused, tag in ops:
+        for c in range(7):
+            opnd(f"L{c}_{tag}", '"=&v"', f"L{tag}[{c}]")
+        for c in range(7):
+            opnd(f"h{c}_{tag}", '"+v"', f"h{tag}[{c}]")
+        opnd(f"cy_{tag}", '"=&s"', f"cy{tag}")
+    opnd("cd", '"=&s"', "cdump")
+    nout = len(ops_e)
+    for s, q, fused, tag in ops:
+        for i in range(4):
+            opnd(f"a{i}_{tag}", '"v"', f"a{tag}.w[{i}]")
+            opnd(f"b{i}_{tag}", '"v"', f"b{tag}.w[{i}]")
+            if fused:
+                opnd(f"c{i}_{tag}", '"v"', f"c{tag}.w[{i}]")
+                opnd(f"d{i}_{tag}", '"v"', f"d{tag}.w[{i}]")
+
+    def ref(x, tag):
+        if isinstance(x, int):
+            return str(x)
+        if x == "cd":
+            return f"%{idx['cd']}"
+        return f"%{idx[f'{x}_{tag}']}"
+
+    # every operation is its own stream (they are independent), so the round-robin spacing grows
+    # with the number of operations and unequal lengths leave only short unpaired tails
+    sched = interleave([[(ins, tag) for ins in product(fused)] for (ss, q, fused, tag) in ops])
+    lines = []
+    for ins, tag in sched:
+        if ins[0] == "nop":
+            lines.append(f"s_nop {ins[1]}")
+        elif ins[0] == "mad":
+            _, d, c, s0, s1, s2 = ins
+            lines.append(f"v_mad_u64_u32 {ref(d, tag)}, {ref(c, tag)}, {ref(s0, tag)}, "
+                         f"{ref(s1, tag)}, {ref(s2, tag)}")
+        else:
+            _, d, c, s0, s1, ci = ins
+            lines.append(f"v_addc_co_u32_e64 {ref(d, tag)}, {ref(c, tag)}, {ref(s0, tag)}, "
+                         f"{ref(s1, tag)}, {ref(ci, tag)}")
+    w("  asm volatile(")
+    for l in lines:
+        w(f'      "{l}\\n\\t"')
+    w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[:nout], ops_e[:nout])))
+    w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[nout:], ops_e[nout:])) + ");")
+    # ---- reductions ----
+    ops_e, cons, idx = [], [], {}
+    for s, q, fused, tag in ops:
+        w(f"  uint32_t l{tag}[7], g{tag}[7];")
+        w(f"  for (int c = 0; c < 7; ++c) {{ l{tag}[c] = (uint32_t)L{tag}[c]; "
+          f"g{tag}[c] = (uint32_t)(L{tag}[c] >> 32); }}")
+        w(f"  uint64_t k{tag}, kk{tag};")
+    for s, q, fused, tag in ops:
+        for c in range(7):
+            opnd(f"l{c}_{tag}", '"+v"', f"l{tag}[{c}]")
+            opnd(f"g{c}_{tag}", '"+v"', f"g{tag}[{c}]")
+            opnd(f"h{c}_{tag}", '"+v"', f"h{tag}[{c}]")
+        for t, reg in ALIAS.items():
+            idx[f"{t}_{tag}"] = idx[f"{reg}_{tag}"]
+        for i in range(4):
+            opnd(f"r{i}_{tag}", '"=&v"', f"r{tag}.w[{i}]")
+        opnd(f"k_{tag}", '"=&s"', f"k{tag}")
+        opnd(f"k2_{tag}", '"=&s"', f"kk{tag}")
+    nout = len(ops_e)
+    opnd("P2", '"v"', "0xFFFFFFE4u")
+
+    def rref(x, tag):
+        if isinstance(x, int):
+            return str(x)
+        if x == "P2":
+            return f"%{idx['P2']}"
+        return f"%{idx[f'{x}_{tag}']}"
+
+    sched = interleave([[(ins, tag) for ins in aliased(reduce_program(fused))]
+                        for (ss, q, fused, tag) in ops])
+    mn = {"add_co": "v_add_co_u32_e64", "addc": "v_addc_co_u32_e64", "sub_co": "v_sub_co_u32_e64",
+          "subb": "v_subb_co_u32_e64"}
+    lines = []
+    for ins, tag in sched:
+        op = ins[0]
+        if op == "nop":
+            lines.append(f"s_nop {ins[1]}")
+        elif op in mn:
+            lines.append(f"{mn[op]} " + ", ".join(rref(x, tag) for x in ins[1:]))
+        elif op == "lsl":
+            lines.append(f"v_lshlrev_b32_e64 {rref(ins[1], tag)}, {ins[2]}, {rref(ins[3], tag)}")
+        elif op == "lsr":
+            lines.append(f"v_lshrrev_b32_e64 {rref(ins[1], tag)}, {ins[2]}, {rref(ins[3], tag)}")
+        elif op == "abit":
+            lines.append(f"v_alignbit_b32 {rref(ins[1], tag)}, {rref(ins[2], tag)}, "
+                         f"{rref(ins[3], tag)}, {ins[4]}")
+        elif op == "cnd":
+            lines.append(f"v_cndmask_b32_e64 {rref(ins[1], tag)}, {rref(ins[2], tag)}, "
+                         f"{rref(ins[3], tag)}, {rref(ins[4], tag)}")
+        else:
+            raise ValueError(op)
+    w("  asm volatile(")
+    for l in lines:
+        w(f'      "{l}\\n\\t"')
+    w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[:nout], ops_e[:nout])))
+    w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[nout:], ops_e[nout:])) + ");")
+    w("}")
+    w("")
+    nops = sum(1 for l in lines if l.startswith("s_nop"))
+    return "\n".join(out), nops
+
+
+FUNCTIONS = {
+    # the Sum FLP query's iterations (prio3_kernels.h sum_query_half): Horner step + gadget-output
+    # fraction step + next y (+ the fraction's denominator when no wire step shares the call)
+    "mont_fma2_mul2": ["F", "F", "M", "M"],
+    "mont_fma2_mul1": ["F", "F", "M"],
+    # wire fraction step + the two denominators
+    "mont_fma1_mul2": ["F", "M", "M"],
+}
+
+
+if __name__ == "__main__":
+    n = check()
+    print(f"simulated {n} single + {n} fused products: ok "
+          f"(single {len(product(False))} + {len(reduce_program(False))}, "
+          f"fused {len(product(True))} + {len(reduce_program(True))} instructions)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "janus_amd", "csrc", "mont_fma.h")
+    parts = ["// GENERATED by tools/gen_mont_fma.py -- edit the generator, not this file.",
+             "// Field128 Montgomery products r = a b 2^-128 and fused sums r = (a b + c d) 2^-128",
+             "// (mod p, inputs < p, outputs canonical), several independent operations issued as",
+             "// interleaved streams; s_nop only where the interleave leaves a carry hazard.",
+             "#pragma once", '#include "field.h"', ""]
+    for name, spec in FUNCTIONS.items():
+        code, nops = gen_function(name, spec)
+        parts.append(f"// streams: {spec}; {nops} s_nop")
+        parts.append(code)
+        print(f"{name}: {spec}, {nops} s_nop")
+    open(path, "w").write("\n".join(parts))
+    print("wrote", path)
