@@ -45,11 +45,11 @@ struct Field128Ops {
   static DEVI F128 half() { return F128{{1u, 0u, 0xFFFFFFF2u, 0x7FFFFFFFu}}; }
 
   static DEVI bool is_canonical(const F128& a) {
-    // a < p  <=>  !(a >= p).  p = [1, 0, P2, P3]
-    if (a.w[3] != P3) return a.w[3] < P3;
-    if (a.w[2] != P2) return a.w[2] < P2;
-    if (a.w[1] != 0u) return false;
-    return a.w[0] < 1u;
+    // a >= p = [1, 0, P2, P3]  <=>  w3 = P3 and (w2 > P2 or (w2 = P2 and (w1, w0) != 0)); written
+    // without short-circuits so it compiles to lane-mask arithmetic, not divergent branches
+    const bool top = a.w[3] == P3, gt2 = a.w[2] > P2, eq2 = a.w[2] == P2;
+    const bool nz = (a.w[1] | a.w[0]) != 0u;
+    return !(top & (gt2 | (eq2 & nz)));
   }
   static DEVI bool eq(const F128& a, const F128& b) {
     return ((a.w[0] ^ b.w[0]) | (a.w[1] ^ b.w[1]) | (a.w[2] ^ b.w[2]) | (a.w[3] ^ b.w[3])) == 0u;

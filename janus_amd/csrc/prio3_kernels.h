@@ -21,6 +21,8 @@
 //   k_accum_*      segmented modular sum of truncated output shares into per-batch aggregates
 //   k_merge        aggregate += other aggregate (mod p) after the RCCL all-gather
 #pragma once
+#include <type_traits>
+
 #include "field.h"
 #include "keccak.h"
 #include "wide.h"
@@ -640,7 +642,15 @@ DEVI uint32_t bitrev(uint32_t x, uint32_t logn) {
 
 template <class FO>
 DEVI typename FO::T ld_tw(const Cfg& cfg, uint32_t i) {
-  return FO::load(cfg.twiddles + (size_t)i * FO::ES);
+  // through the constant address space: a wave-uniform index becomes a scalar load (s_load_dwordx4),
+  // so no vector-memory wait (vmcnt) is spent on the tables -- one would also wait for the LDS-DMA
+  // fills in flight
+  using CP = const __attribute__((address_space(4))) uint32_t*;
+  const CP p = (CP)(cfg.twiddles + (size_t)i * FO::ES);
+  typename FO::T v;
+#pragma unroll
+  for (int k = 0; k < FO::ES / 4; ++k) v.w[k] = p[k];
+  return v;
 }
 
 // Two in-place radix-2 DIT NTTs of size m (inputs already bit-reversed) over LDS arrays A and B,
@@ -862,62 +872,119 @@ DEVI typename FO::T inv_mont(const typename FO::T& x) {
   else return inv_mont64(x);
 }
 
-// Sum's FLP query when calls = m/2 (power-of-two bits) and r^m != 1, Field128, one lane per report:
-// the same field values as the generic loop below, from fewer products:
-//   * the gadget-output sum  v = sum_i F_i G(y_i),  y_i = r alpha^i,  G(y) = y (y^calls - 1)/(y - 1):
-//     y_i^calls = r^calls (-1)^i =: s_i, so with c_par = s_i - 1 (two constants) and
-//     y/(y - 1) = 1 + 1/(y - 1):   v = sum_par c_par (sum_(i = par) F_i + sum_(i = par) F_i/(y_i - 1))
-//     -- two running fractions N/D (even and odd i) updated as N e + F D (ONE fused product),
-//     D e, plus a plain sum of F;
-//   * the wire  sum_(k=0..calls) alpha^k x_k/(t - alpha^k) = t sum_k x_k/(t - alpha^k) - sum_k x_k
-//     (alpha^k/(t - alpha^k) = t/(t - alpha^k) - 1): the running fraction N d + x D (fused), D d, no
-//     alpha^k x product; k = 0 (x_0 = the proof seed) is iteration i = 0;
-//   * p(t) = sum_i (c_i + t^m c_(i+m)) t^i as ONE fused product t pt + t^m c_(i+m) per i;
+// Sum's FLP query when calls = m/2 (power-of-two bits, m >= 4) and r^m != 1, Field128, one lane
+// per report: the same field values as the generic loop below, from fewer products.  With
+// h = m/2 = calls, alpha^h = -1, beta_i = alpha^-i (tables, Montgomery):
+//   * gadget-output sum  v = sum_i F_i G(y_i),  F_i = c_i + c_(i+m),  y_i = r alpha^i,
+//     G(y) = y (y^calls - 1)/(y - 1).  y_i^calls = r^calls (-1)^i =: s_i and
+//     y_i/(y_i - 1) = r/(r - beta_i), so  v = r sum_par c_par Q_par,  c_par = s_par - 1,
+//     Q_par = sum_(i = par) F_i/(r - beta_i): the denominators are r minus a constant.  Pairing
+//     i with j = i + h (same parity, beta_j = -beta_i):
+//       F_i/(r - beta) + F_j/(r + beta) = (r (F_i + F_j) + beta (F_i - F_j)) / (r^2 - beta^2),
+//     so each of the h iterations adds ONE pair to its parity's fraction N/D;
+//   * the wire  sum_(k=0..calls) alpha^k x_k/(t - alpha^k) = t sum_k x_k/(t - alpha^k) - sum_k x_k:
+//     iteration i takes k = i (x_0 = the proof seed), k = calls is the fraction's start;
+//   * p(t) = sum_(i<h) (A_i + t^h A_(i+h)) t^i,  A_i = c_i + t^m c_(i+m): one Horner step per pair;
 //   * the three denominators share one inversion.
-// Products issue as interleaved fused / single Montgomery streams (mont_fma.h): per iteration
-// 2 fused + 2 single (non-wire i) or 3 fused + 3 single (wire i) against 8 / 12 products before.
+// Per iteration 5 fused + 2 single Montgomery products (mont_fma.h, two interleaved calls)
+// against 5 + 5 for two iterations of the unpaired form (gadget fraction over y_i - 1 with y_i
+// advanced by a product) and 8 + 16 products of the mul3 loop.
 // Domains: values marked M are Montgomery form (x R), the rest plain; mont(M, plain) is plain.
-DEVI void sum_query_half(const Cfg& cfg, const F128& tm, const F128& tmm, const F128& rm,
-                         const F128& rc, const uint8_t* gp, const uint8_t* xr, const F128& s0,
+// Operands: iteration i reads c_i, c_(i+m), c_(i+h), c_(i+h+m) (gadget coefficients, proof
+// elements 1 + .) and x_i (measurement element i - 1; x_0 = the proof seed).  A loop trip (odd i,
+// then i - 1) takes two consecutive elements of each of these five streams, which arrive by LDS-DMA
+// into a per-wave window of 5 x 2 KB (kSqWin): instruction k of a stream fills 1 KB = 32 reports x
+// 2 elements, slot 2q + (u ^ ((q >> 2) & 1)) holding element u of report q (each lane's
+// ds_read_b128 of its own report is then bank-conflict-free).  The next trip's DMA is issued once
+// the second iteration's operands sit in registers, so it lands under that iteration's products
+// and no VGPRs are held by loads in flight.  Every lane of the wave takes part (dead lanes compute
+// on a clamped row).
+constexpr uint32_t kSqWin = 5u * 2048u;  // bytes per wave
+
+DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane, CRows meas,
+                         CRows proof, uint8_t* win, const F128& tm, const F128& th,
+                         const F128& tmm, const F128& rm, const F128& rc, const F128& s0,
                          bool& bad, F128& pt_out, F128& w0_out, F128& v_out) {
   using FO = Field128Ops;
   using T = F128;
-  const uint32_t m = cfg.m, calls = cfg.calls, gp_len = cfg.gp_len;
+  const uint32_t m = cfg.m, h = cfg.calls, gp_len = cfg.gp_len;
   const T one = FO::one_mont();
-  T pt = FO::zero();                      // Horner, plain
-  T N[2] = {FO::zero(), FO::zero()};      // v fractions (even, odd i), plain
-  T D[2] = {one, one};                    // their denominators, M
-  T S[2] = {FO::zero(), FO::zero()};      // sums of F by parity, plain
-  T Nw = FO::zero(), Dw = one, X = FO::zero();  // wire fraction (plain / M) and sum x (plain)
-  T y = FO::mul(rm, ld_tw<FO>(cfg, m - 1u));     // y_(m-1), M
-  for (uint32_t i = m - 1;; --i) {
-    const T ci = FO::load(gp + (size_t)i * 16);
-    const T ch = i + m < gp_len ? FO::load(gp + (size_t)(i + m) * 16) : FO::zero();
-    bad |= !FO::is_canonical(ci) || !FO::is_canonical(ch);
-    const T f = FO::add(ci, ch);
-    const T e = FO::sub(y, one);                       // M(y - 1)
-    const uint32_t par = i & 1u;                       // loop-uniform
-    S[par] = FO::add(S[par], f);
-    const T twn = ld_tw<FO>(cfg, i ? i - 1u : 0u);      // alpha^(i-1): the next y
-    T PQ, VN, yn, VD;
-    if (i <= calls) {  // wire term k = i (x_0 = the proof seed)
-      const T x = i ? FO::load(xr + (size_t)(i - 1) * 16) : s0;
-      if (i) bad |= !FO::is_canonical(x);
-      X = FO::add(X, x);
-      const T d = FO::sub(tm, ld_tw<FO>(cfg, i));       // M(t - alpha^i)
-      mont_fma2_mul1(tm, pt, tmm, ch, PQ, N[par], e, f, D[par], VN, rm, twn, yn);
-      T NW, DW;
-      mont_fma1_mul2(Nw, d, x, Dw, NW, Dw, d, DW, D[par], e, VD);
-      Nw = NW;
-      Dw = DW;
-    } else {
-      mont_fma2_mul2(tm, pt, tmm, ch, PQ, N[par], e, f, D[par], VN, rm, twn, yn, D[par], e, VD);
+  const T t3h = FO::mul(tmm, th);                    // M(t^(m + h))
+  const T r2 = FO::mul(rm, rm);                      // M(r^2)
+  // DMA of the trip whose first (odd) iteration is i: elements i - 1, i of the five streams
+  auto stage = [&](uint32_t i) {
+    uint32_t ln;  // opaque copy: the row addresses are recomputed per trip, never held
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    const uint32_t e = i - 1u + ((ln & 1u) ^ ((ln >> 3) & 1u));  // this lane's element
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+      const uint32_t row = min(r0w + 32u * k + (ln >> 1), n - 1u);
+      const uint8_t* pr = proof.base + (size_t)row * proof.stride;
+      const uint8_t* xr = meas.base + (size_t)row * meas.stride;
+      const uint32_t off[4] = {e, e + m, e + h, (uint32_t)min(e + h + m, gp_len - 1u)};
+#pragma unroll
+      for (uint32_t s = 0; s < 4; ++s)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(pr + 16u * (1u + off[s])),
+            (__attribute__((address_space(3))) void*)(win + 2048u * s + 1024u * k), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(xr + 16u * (e ? e - 1u : 0u)),
+          (__attribute__((address_space(3))) void*)(win + 2048u * 4u + 1024u * k), 16, 0, 0);
     }
-    pt = FO::add(PQ, ci);
-    N[par] = VN;
-    D[par] = VD;
-    y = yn;
-    if (i == 0) break;
+  };
+  const uint32_t sl = 32u * lane, sw = (lane >> 2) & 1u;
+  auto rd = [&](uint32_t s, uint32_t u) { return FO::load(win + 2048u * s + sl + 16u * (u ^ sw)); };
+  T N[2] = {FO::zero(), FO::zero()};                 // gadget-output fractions by parity, plain
+  T D[2] = {one, one};                               // their denominators, M
+  T X = FO::load(meas.at(min(r0w + lane, n - 1u)) + (size_t)(h - 1) * 16);  // x_calls
+  bad |= !FO::is_canonical(X);
+  T Nw = X, Dw = FO::sub(tm, ld_tw<FO>(cfg, h));     // plain / M(t - alpha^calls)
+  // Horner's p_(i+1) = P1 + P2 + c_(i+1) is finished inside iteration i's additions
+  T P1 = FO::zero(), P2 = FO::zero(), cprev = FO::zero();
+  stage(h - 1u);
+  auto step = [&](uint32_t i, auto PAR) {
+    constexpr uint32_t par = decltype(PAR)::value;  // = i & 1 = the window slot
+    if (par) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this trip's window has landed
+    const T ci = rd(0, par), cim = rd(1, par), cj = rd(2, par);
+    const T cjm = i + h + m < gp_len ? rd(3, par) : FO::zero();
+    const T x = i ? rd(4, par) : s0;
+    if (!par && i) {  // operands of the trip in registers: the window is free for the next one
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stage(i - 1u);
+    }
+    bad |= !FO::is_canonical(ci) | !FO::is_canonical(cim) | !FO::is_canonical(cj) |
+           !FO::is_canonical(cjm) | !FO::is_canonical(x);
+    const uint32_t mi = (m - i) & (m - 1u), m2i = (m - 2u * i) & (m - 1u);
+    const T beta = ld_tw<FO>(cfg, mi);                              // M(alpha^-i)
+    T fi, fj, d2, dw, S;
+    // F_i, F_j, M(r^2 - beta^2), M(t - alpha^i), P1 + P2
+    modaddsub_AASSA(ci, cim, fi, cj, cjm, fj, r2, ld_tw<FO>(cfg, m2i), d2, tm, ld_tw<FO>(cfg, i),
+                    dw, P1, P2, S);
+    T fs, fd, Xn, pt;
+    modaddsub_ASAA(fi, fj, fs, fi, fj, fd, X, x, Xn, S, cprev, pt);
+    T U, DN;
+    mont_fma3_mul1(tm, pt, tmm, cim, P1, th, cj, t3h, cjm, P2, rm, fs, beta, fd, U, D[par], d2,
+                   DN);
+    T NN, NW, DW;
+    mont_fma2_mul1(N[par], d2, U, D[par], NN, Nw, dw, x, Dw, NW, Dw, dw, DW);
+    N[par] = NN;
+    D[par] = DN;
+    Nw = NW;
+    Dw = DW;
+    X = Xn;
+    cprev = ci;
+  };
+  // h is even: the pairs (odd i, even i - 1) unroll with constant parity
+  for (uint32_t i = h - 1;; i -= 2) {
+    step(i, std::integral_constant<uint32_t, 1>{});
+    step(i - 1, std::integral_constant<uint32_t, 0>{});
+    if (i == 1) break;
+  }
+  T pt;
+  {
+    T S;
+    modaddsub_A(P1, P2, S);
+    modaddsub_A(S, cprev, pt);
   }
   // one inversion for Dw, D0, D1
   T t1, t2, t3;
@@ -930,9 +997,9 @@ DEVI void sum_query_half(const Cfg& cfg, const F128& tm, const F128& tmm, const 
   const T cm = FO::mul(FO::sub(tmm, one), ld_tw<FO>(cfg, m));  // M((t^m - 1)/m)
   const T c0 = FO::sub(rc, one), c1 = FO::sub(FO::sub(FO::zero(), rc), one);  // M(s_par - 1)
   T tq, v0, v1;
-  mul3<FO>(tm, qw, c0, FO::add(S[0], q0), c1, FO::add(S[1], q1), tq, v0, v1);
+  mul3<FO>(tm, qw, c0, q0, c1, q1, tq, v0, v1);
   w0_out = FO::mul(cm, FO::sub(tq, X));
-  v_out = FO::add(v0, v1);
+  v_out = FO::mul(rm, FO::add(v0, v1));
   pt_out = pt;
 }
 
@@ -946,27 +1013,36 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
                                                         uint8_t* status) {
   using T = typename FO::T;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  if (status[r] != ST_OK) return;
+  const bool live = r < n && status[r] == ST_OK;
+  // Sum with calls = m/2 (Field128): the paired query, whole waves (its operands arrive by
+  // LDS-DMA for all 64 lanes); every other shape: one independent lane per live report
+  bool pair = false;
+  if constexpr (FO::ES == 16)
+    pair = cfg.kind == KIND_SUM && 2u * cfg.calls == cfg.m && cfg.m >= 4u && cfg.arity == 1u;
+  if (!pair && !live) return;
+  const uint32_t lane = threadIdx.x & 63u, r0w = r - lane;
+  if (pair && r0w >= n) return;  // wave-uniform
+  const uint32_t rr = r < n ? r : n - 1u;  // = r on the generic path
   const size_t ES = FO::ES;
   const uint32_t m = cfg.m, calls = cfg.calls, arity = cfg.arity, gp_len = cfg.gp_len;
-  const uint8_t* xr = meas.at(r);
-  const uint8_t* pr = proof.at(r);
+  const uint8_t* xr = meas.at(rr);
+  const uint8_t* pr = proof.at(rr);
   const uint8_t* gp = pr + (size_t)arity * ES;  // gadget poly coefficients
   bool bad = false;
   const T one = FO::one_mont();
-  const T tm = FO::to_mont(FO::load(tq.at(r)));
+  const T tm = FO::to_mont(FO::load(tq.at(rr)));
   T tmm = tm;
   // Sum: t^m, r^m and r^calls (calls < m, right-to-left square-and-multiply) advance together,
   // one triple of squarings per bit
-  T rm = FO::zero(), rmm = FO::zero(), rc = one;
+  T rm = FO::zero(), rmm = FO::zero(), rc = one, th = tm;
   if (cfg.kind == KIND_SUM) {
-    rm = FO::to_mont(FO::load(jr.at(r)));
+    rm = FO::to_mont(FO::load(jr.at(rr)));
     rmm = rm;
     T b = rm;
     for (uint32_t q = 0; q < cfg.logm; ++q) {
       if ((calls >> q) & 1u) rc = FO::mul(rc, b);
       mul3<FO>(tmm, tmm, rmm, rmm, b, b, tmm, rmm, b);
+      if (q + 2u == cfg.logm) th = tmm;  // t^(m/2)
     }
   } else {
     for (uint32_t i = 0; i < cfg.logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
@@ -978,6 +1054,30 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
   T nw0 = FO::zero(), nw1 = FO::zero(), dw = one;
   const T s0 = FO::load(pr), s1 = arity > 1 ? FO::load(pr + ES) : FO::zero();
   bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
+  if constexpr (FO::ES == 16) {
+    if (pair) {
+      __shared__ __attribute__((aligned(16))) uint8_t sqlds[4 * kSqWin];
+      const bool r_root = FO::eq(rmm, one);  // y_i = 1 for some i: the generic loop below
+      bool pbad = bad;
+      T pt, w0, v;
+      sum_query_pair(cfg, n, r0w, lane, meas, proof, sqlds + (threadIdx.x >> 6) * kSqWin, tm, th,
+                     tmm, rm, rc, s0, pbad, pt, w0, v);
+      if (!live) return;
+      if (!r_root) {
+        uint8_t* outp = out_prep.at(r);
+        FO::store(outp, v);
+        FO::store(outp + ES, w0);
+        FO::store(outp + (size_t)(1 + arity) * ES, pt);
+        const uint8_t* pp = part.at(r);
+        uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
+        st64(dst, ld64(pp));
+        st64(dst + 8, ld64(pp + 8));
+        if (pbad) status[r] = ST_INVALID_MESSAGE;
+        else if (root) status[r] = ST_VDAF_PREP_ERROR;
+        return;
+      }
+    }
+  }
   T x0 = FO::zero();
   if (cfg.kind == KIND_COUNT) {
     x0 = FO::load(xr);
@@ -1029,27 +1129,7 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
       vn = FO::add(FO::mul(vn, e), FO::mul(b, vd));
       vd = FO::mul(vd, e);
     };
-    bool done = false;
-    if constexpr (FO::ES == 16) {
-      if (!r_root && 2u * calls == m && arity == 1) {
-        T w0, v;
-        sum_query_half(cfg, tm, tmm, rm, rc, gp, xr, s0, bad, pt, w0, v);
-        uint8_t* outp = out_prep.at(r);
-        FO::store(outp, v);
-        FO::store(outp + ES, w0);
-        FO::store(outp + (size_t)(1 + arity) * ES, pt);
-        const uint8_t* pp = part.at(r);
-        uint8_t* dst = outp + (size_t)cfg.verifier_len * ES;
-        st64(dst, ld64(pp));
-        st64(dst + 8, ld64(pp + 8));
-        if (bad) status[r] = ST_INVALID_MESSAGE;
-        else if (root) status[r] = ST_VDAF_PREP_ERROR;
-        done = true;
-      }
-    }
-    if (done) {
-      return;
-    } else if (!r_root && FLPQ_MUL3) {
+    if (!r_root && FLPQ_MUL3) {
       // the same three chains, every iteration's products issued as hazard-free triples
       // (mont_mul3, Field128).  b_i * vd is refactored as (y f) * ((yc - 1) vd) so the
       // 12 (13) products of a wire iteration form 4 triples (+1 single); when calls == m / 2

@@ -36,7 +36,7 @@ def product(fused):
     2^(32 c + 64)).  Each mad's carry is read by the addc right after it (the interleave or the
     emitter's s_nop gives the wait states)."""
     ins = []
-    first = set()
+    first, hset = set(), set()
     pairs = [("a", "b")] + ([("c", "d")] if fused else [])
     for (x, y) in pairs:
         for c in range(7):
@@ -49,12 +49,17 @@ def product(fused):
                     ins.append(("mad", f"L{c}", "cd", f"{x}{i}", f"{y}{j}", 0))
                 else:
                     ins.append(("mad", f"L{c}", "cy", f"{x}{i}", f"{y}{j}", f"L{c}"))
-                    ins.append(("addc", f"h{c}", "cd", f"h{c}", 0, "cy"))
+                    # the first carry into h_c sets it (h_c = 0 + 0 + carry), later ones add
+                    ins.append(("addc", f"h{c}", "cd", f"h{c}" if c in hset else 0, 0, "cy"))
+                    hset.add(c)
     return ins
 
 
-def product_inits():
-    return [f"h{c}" for c in range(7)]  # zero-initialised carry words
+def product_inits(fused):
+    """carry words no mad of the product writes (a single product's outer columns hold one
+    partial product each): zero-initialised in C, the rest are pure asm outputs"""
+    written = {ins[1] for ins in product(fused) if ins[0] == "addc"}
+    return [f"h{c}" for c in range(7) if f"h{c}" not in written]
 
 
 def reduce_program(fused):
@@ -158,6 +163,10 @@ def simulate(prog, st):
             st[ins[1]] = (((val(st, ins[2]) << 32) | val(st, ins[3])) >> ins[4]) & M32
         elif op == "cnd":
             st[ins[1]] = val(st, ins[3]) if st[ins[4]] else val(st, ins[2])
+        elif op == "vsub":
+            st[ins[1]] = (val(st, ins[2]) - val(st, ins[3])) & M32
+        elif op == "and":
+            st[ins[1]] = val(st, ins[2]) & val(st, ins[3])
         elif op == "nop":
             pass
         else:
@@ -173,7 +182,9 @@ def run_op(fused, a, b, c=0, d=0):
     for i in range(4):
         st[f"a{i}"], st[f"b{i}"] = (a >> (32 * i)) & M32, (b >> (32 * i)) & M32
         st[f"c{i}"], st[f"d{i}"] = (c >> (32 * i)) & M32, (d >> (32 * i)) & M32
-    for h in product_inits():
+    for c in range(7):
+        st[f"h{c}"] = 0xDEADBEEF  # garbage: only product_inits are zeroed
+    for h in product_inits(fused):
         st[h] = 0
     simulate(product(fused), st)
     for k in range(7):
@@ -264,14 +275,17 @@ def gen_function(name, spec):
 
     for s, q, fused, tag in ops:
         w(f"  uint64_t L{tag}[7];")
-        w(f"  uint32_t h{tag}[7] = {{0u, 0u, 0u, 0u, 0u, 0u, 0u}};")
+        w(f"  uint32_t h{tag}[7];")
+        for h in product_inits(fused):
+            w(f"  h{tag}[{h[1:]}] = 0u;")
         w(f"  uint64_t cy{tag};")
     w("  uint64_t cdump;")
     for s, q, fused, tag in ops:
         for c in range(7):
             opnd(f"L{c}_{tag}", '"=&v"', f"L{tag}[{c}]")
+        zero = product_inits(fused)
         for c in range(7):
-            opnd(f"h{c}_{tag}", '"+v"', f"h{tag}[{c}]")
+            opnd(f"h{c}_{tag}", '"+v"' if f"h{c}" in zero else '"=&v"', f"h{tag}[{c}]")
         opnd(f"cy_{tag}", '"=&s"', f"cy{tag}")
     opnd("cd", '"=&s"', "cdump")
     nout = len(ops_e)
@@ -372,13 +386,147 @@ def gen_function(name, spec):
     return "\n".join(out), nops
 
 
+# ---------------------------------------------------------------------------------------------
+# modular additions / subtractions (inputs < p, outputs canonical), c = 2^128 - p = [-1, -1, 27, 0]
+# ---------------------------------------------------------------------------------------------
+def modadd_program():
+    """r = a + b mod p: s = a + b (carry k1); k2 = carry of s + c; sel = k1 + k2 (they exclude
+    each other: k1 = 1 means s - 2^128 < p - c); r = s + (c & -sel) mod 2^128.  16 VALU."""
+    ins = [("add_co", "r0", "k", "a0", "b0")]
+    for i in range(1, 4):
+        ins.append(("addc", f"r{i}", "k", f"a{i}", f"b{i}", "k"))
+    ins.append(("addc", "q", "k", 0, 0, "k"))  # q = k1
+    ins.append(("add_co", "x", "k", "r0", -1))
+    ins.append(("addc", "x", "k", "r1", -1, "k"))
+    ins.append(("addc", "x", "k", "r2", 27, "k"))
+    ins.append(("addc", "x", "k", "r3", 0, "k"))
+    ins.append(("addc", "q", "k", "q", 0, "k"))  # q = k1 + k2
+    ins.append(("vsub", "m", 0, "q"))
+    ins.append(("and", "x", 27, "m"))
+    ins.append(("add_co", "r0", "k", "r0", "m"))
+    ins.append(("addc", "r1", "k", "r1", "m", "k"))
+    ins.append(("addc", "r2", "k", "r2", "x", "k"))
+    ins.append(("addc", "r3", "k", "r3", 0, "k"))
+    return ins
+
+
+def modsub_program():
+    """r = a - b mod p: d = a - b (borrow k); r = d - (c & -k) mod 2^128 (= d + p - 2^128).
+    10 VALU."""
+    ins = [("sub_co", "r0", "k", "a0", "b0")]
+    for i in range(1, 4):
+        ins.append(("subb", f"r{i}", "k", f"a{i}", f"b{i}", "k"))
+    ins.append(("subb", "m", "k", 0, 0, "k"))  # m = -borrow
+    ins.append(("and", "x", 27, "m"))
+    ins.append(("sub_co", "r0", "k", "r0", "m"))
+    ins.append(("subb", "r1", "k", "r1", "m", "k"))
+    ins.append(("subb", "r2", "k", "r2", "x", "k"))
+    ins.append(("subb", "r3", "k", "r3", 0, "k"))
+    return ins
+
+
+def run_addsub(kind, a, b):
+    st = {}
+    for i in range(4):
+        st[f"a{i}"], st[f"b{i}"] = (a >> (32 * i)) & M32, (b >> (32 * i)) & M32
+    simulate(modadd_program() if kind == "A" else modsub_program(), st)
+    return sum(st[f"r{i}"] << (32 * i) for i in range(4))
+
+
+def check_addsub(trials=20000):
+    rng = random.Random(11)
+    edge = [0, 1, 2, P - 1, P - 2, P // 2, P // 2 + 1, (1 << 128) - 28 * (1 << 64), 1 << 127,
+            28 * (1 << 64) - 1, 28 * (1 << 64)]
+    pick = lambda t, k: rng.choice(edge) if t % k == 0 else rng.randrange(P)
+    for t in range(trials):
+        a, b = pick(t, 3), pick(t, 2)
+        assert run_addsub("A", a, b) == (a + b) % P, (a, b)
+        assert run_addsub("S", a, b) == (a - b) % P, (a, b)
+    for a in edge:
+        for b in edge:
+            assert run_addsub("A", a, b) == (a + b) % P and run_addsub("S", a, b) == (a - b) % P
+    return trials
+
+
+def gen_addsub(name, spec):
+    """spec: a string of "A" (r = a + b) / "S" (r = a - b) operations, one stream each, issued
+    round-robin in one asm statement.  Signature: (a, b, r) per operation."""
+    ops = [(q, kind, f"{q}") for q, kind in enumerate(spec)]
+    out = []
+    w = out.append
+    params = []
+    for q, kind, tag in ops:
+        params += [f"const F128& a{tag}", f"const F128& b{tag}", f"F128& r{tag}"]
+    w(f"DEVI void {name}(" + ", ".join(params) + ") {")
+    ops_e, cons, idx = [], [], {}
+
+    def opnd(key, con, expr):
+        idx[key] = len(ops_e)
+        ops_e.append(expr)
+        cons.append(con)
+
+    for q, kind, tag in ops:
+        w(f"  uint32_t x{tag}, m{tag}" + (f", q{tag};" if kind == "A" else ";"))
+        w(f"  uint64_t k{tag};")
+    for q, kind, tag in ops:
+        for i in range(4):
+            opnd(f"r{i}_{tag}", '"=&v"', f"r{tag}.w[{i}]")
+        opnd(f"x_{tag}", '"=&v"', f"x{tag}")
+        opnd(f"m_{tag}", '"=&v"', f"m{tag}")
+        if kind == "A":
+            opnd(f"q_{tag}", '"=&v"', f"q{tag}")
+        opnd(f"k_{tag}", '"=&s"', f"k{tag}")
+    nout = len(ops_e)
+    for q, kind, tag in ops:
+        for i in range(4):
+            opnd(f"a{i}_{tag}", '"v"', f"a{tag}.w[{i}]")
+            opnd(f"b{i}_{tag}", '"v"', f"b{tag}.w[{i}]")
+
+    def ref(x, tag):
+        return str(x) if isinstance(x, int) else f"%{idx[f'{x}_{tag}']}"
+
+    progs = [[(ins, tag) for ins in (modadd_program() if kind == "A" else modsub_program())]
+             for (q, kind, tag) in ops]
+    mn = {"add_co": "v_add_co_u32_e64", "addc": "v_addc_co_u32_e64", "sub_co": "v_sub_co_u32_e64",
+          "subb": "v_subb_co_u32_e64"}
+    lines = []
+    for ins, tag in interleave(progs):
+        op = ins[0]
+        if op == "nop":
+            lines.append(f"s_nop {ins[1]}")
+        elif op in mn:
+            lines.append(f"{mn[op]} " + ", ".join(ref(x, tag) for x in ins[1:]))
+        elif op == "vsub":
+            lines.append(f"v_sub_u32_e64 {ref(ins[1], tag)}, {ref(ins[2], tag)}, {ref(ins[3], tag)}")
+        elif op == "and":
+            lines.append(f"v_and_b32_e64 {ref(ins[1], tag)}, {ref(ins[2], tag)}, {ref(ins[3], tag)}")
+        else:
+            raise ValueError(op)
+    w("  asm volatile(")
+    for l in lines:
+        w(f'      "{l}\\n\\t"')
+    w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[:nout], ops_e[:nout])))
+    w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[nout:], ops_e[nout:])) + ");")
+    w("}")
+    w("")
+    nops = sum(1 for l in lines if l.startswith("s_nop"))
+    return "\n".join(out), nops
+
+
+# one iteration of the Sum FLP query's additions (prio3_kernels.h sum_query_pair)
+ADDSUB = {
+    "modaddsub_AASSA": "AASSA",  # F_i, F_j, r^2 - beta^2, t - alpha^i, the two Horner halves
+    "modaddsub_ASAA": "ASAA",    # F_i + F_j, F_i - F_j, X + x, Horner + c_(i+1)
+    "modaddsub_A": "A",
+}
+
+
 FUNCTIONS = {
-    # the Sum FLP query's iterations (prio3_kernels.h sum_query_half): Horner step + gadget-output
-    # fraction step + next y (+ the fraction's denominator when no wire step shares the call)
-    "mont_fma2_mul2": ["F", "F", "M", "M"],
+    # one iteration of the Sum FLP query (prio3_kernels.h sum_query_pair), two calls:
+    #   the two Horner halves + the paired numerator + the gadget-output denominator,
+    "mont_fma3_mul1": ["F", "F", "F", "M"],
+    #   then the gadget-output fraction's numerator + the wire fraction (numerator, denominator)
     "mont_fma2_mul1": ["F", "F", "M"],
-    # wire fraction step + the two denominators
-    "mont_fma1_mul2": ["F", "M", "M"],
 }
 
 
@@ -396,6 +544,15 @@ if __name__ == "__main__":
              "#pragma once", '#include "field.h"', ""]
     for name, spec in FUNCTIONS.items():
         code, nops = gen_function(name, spec)
+        parts.append(f"// streams: {spec}; {nops} s_nop")
+        parts.append(code)
+        print(f"{name}: {spec}, {nops} s_nop")
+    n = check_addsub()
+    print(f"simulated {n} modular additions + subtractions: ok "
+          f"({len(modadd_program())} / {len(modsub_program())} instructions)")
+    parts.append("// modular additions (A) / subtractions (S), one stream each")
+    for name, spec in ADDSUB.items():
+        code, nops = gen_addsub(name, spec)
         parts.append(f"// streams: {spec}; {nops} s_nop")
         parts.append(code)
         print(f"{name}: {spec}, {nops} s_nop")
