@@ -25,6 +25,11 @@ struct F128 {
 struct F64 {
   uint32_t w[2];
 };
+#include "modadd.h"  // f128_add_chain / f128_sub_chain / f128_mont_mul1 (generated)
+
+#ifndef P3G_ADD_CPP
+#define P3G_ADD_CPP 0  // A/B: 1 = Field128 add / sub / mul in plain C++ (64-bit temporaries)
+#endif
 
 // ----------------------------------------------------------------------------------------------
 // Field128
@@ -59,6 +64,11 @@ struct Field128Ops {
   // a + b mod p.  With c = 2^128 - p = [FFFFFFFF, FFFFFFFF, 1B, 0]:
   //   s = a + b (carry k1);  u = s + c (carry k2);  result = (k1|k2) ? u : s.
   static DEVI F128 add(const F128& a, const F128& b) {
+    if constexpr (!P3G_ADD_CPP) {
+      F128 r;
+      f128_add_chain(a, b, r);
+      return r;
+    }
     uint64_t t;
     uint32_t s0, s1, s2, s3, k1;
     t = (uint64_t)a.w[0] + b.w[0];            s0 = (uint32_t)t;
@@ -75,6 +85,11 @@ struct Field128Ops {
   }
   // a - b mod p: d = a - b (borrow) ; if borrow: d += p
   static DEVI F128 sub(const F128& a, const F128& b) {
+    if constexpr (!P3G_ADD_CPP) {
+      F128 r;
+      f128_sub_chain(a, b, r);
+      return r;
+    }
     int64_t t;
     uint32_t d0, d1, d2, d3;
     uint64_t u;
@@ -99,6 +114,11 @@ struct Field128Ops {
   // that needs no multiplier: p = 1 + (2^64 - 28) 2^64, so -p^-1 = -1 mod 2^64 (m = -t0) and
   // m * p / 2^64 = [ -28m (low word), +m (next word) ] after the exact division.
   static DEVI F128 mul(const F128& a, const F128& b) {
+    if constexpr (!P3G_ADD_CPP) {
+      F128 r;
+      f128_mont_mul1(a, b, r);
+      return r;
+    }
     typedef unsigned __int128 u128;
     const uint64_t alo = ((uint64_t)a.w[1] << 32) | a.w[0], ahi = ((uint64_t)a.w[3] << 32) | a.w[2];
     const uint64_t blo = ((uint64_t)b.w[1] << 32) | b.w[0], bhi = ((uint64_t)b.w[3] << 32) | b.w[2];

@@ -248,7 +248,7 @@ def interleave(streams):
     return out
 
 
-def gen_function(name, spec):
+def gen_function(name, spec, volatile=True):
     """spec: one string per stream of "F" (fused) / "M" (single) operations, e.g. ["F", "F", "MM"].
     Signature: for every operation in stream order, (a, b[, c, d]) inputs then its output."""
     ops = []  # (stream, op index in stream, fused, tag)
@@ -319,7 +319,7 @@ def gen_function(name, spec):
             _, d, c, s0, s1, ci = ins
             lines.append(f"v_addc_co_u32_e64 {ref(d, tag)}, {ref(c, tag)}, {ref(s0, tag)}, "
                          f"{ref(s1, tag)}, {ref(ci, tag)}")
-    w("  asm volatile(")
+    w("  asm volatile(" if volatile else "  asm(")
     for l in lines:
         w(f'      "{l}\\n\\t"')
     w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[:nout], ops_e[:nout])))
@@ -375,7 +375,7 @@ def gen_function(name, spec):
                          f"{rref(ins[3], tag)}, {rref(ins[4], tag)}")
         else:
             raise ValueError(op)
-    w("  asm volatile(")
+    w("  asm volatile(" if volatile else "  asm(")
     for l in lines:
         w(f'      "{l}\\n\\t"')
     w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[:nout], ops_e[:nout])))
@@ -448,9 +448,10 @@ def check_addsub(trials=20000):
     return trials
 
 
-def gen_addsub(name, spec):
+def gen_addsub(name, spec, volatile=True):
     """spec: a string of "A" (r = a + b) / "S" (r = a - b) operations, one stream each, issued
-    round-robin in one asm statement.  Signature: (a, b, r) per operation."""
+    round-robin in one asm statement.  Signature: (a, b, r) per operation.  volatile=False leaves
+    the compiler free to schedule / drop the statement like any pure expression."""
     ops = [(q, kind, f"{q}") for q, kind in enumerate(spec)]
     out = []
     w = out.append
@@ -502,7 +503,7 @@ def gen_addsub(name, spec):
             lines.append(f"v_and_b32_e64 {ref(ins[1], tag)}, {ref(ins[2], tag)}, {ref(ins[3], tag)}")
         else:
             raise ValueError(op)
-    w("  asm volatile(")
+    w("  asm volatile(" if volatile else "  asm(")
     for l in lines:
         w(f'      "{l}\\n\\t"')
     w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[:nout], ops_e[:nout])))
@@ -556,5 +557,23 @@ if __name__ == "__main__":
         parts.append(f"// streams: {spec}; {nops} s_nop")
         parts.append(code)
         print(f"{name}: {spec}, {nops} s_nop")
+    open(path, "w").write("\n".join(parts))
+    print("wrote", path)
+    # Field128Ops::add / sub (field.h): one operation, s_nop where its own chain needs them
+    path = os.path.join(root, "janus_amd", "csrc", "modadd.h")
+    parts = ["// GENERATED by tools/gen_mont_fma.py -- edit the generator, not this file.",
+             "// Field128 r = a + b / a - b mod p and r = a b 2^-128 mod p (inputs < p, outputs canonical) as",
+             "// 32-bit carry chains; included by field.h for Field128Ops::add / sub / mul.",
+             "#pragma once", ""]
+    for name, spec in {"f128_add_chain": "A", "f128_sub_chain": "S"}.items():
+        code, nops = gen_addsub(name, spec, volatile=False)
+        parts.append(f"// {nops} s_nop")
+        parts.append(code)
+        print(f"{name}: {spec}, {nops} s_nop")
+    # Field128Ops::mul: one Montgomery product
+    code, nops = gen_function("f128_mont_mul1", ["M"], volatile=False)
+    parts.append(f"// one Montgomery product; {nops} s_nop")
+    parts.append(code)
+    print(f"f128_mont_mul1: {nops} s_nop")
     open(path, "w").write("\n".join(parts))
     print("wrote", path)
