@@ -653,6 +653,15 @@ DEVI typename FO::T ld_tw(const Cfg& cfg, uint32_t i) {
   return v;
 }
 
+// 16-byte LDS store the compiler's wait-count pass does not see (see k_flp_weights' put); the
+// caller orders it against LDS-DMA fills and reads of the same bytes with explicit s_waitcnt
+DEVI void lds_store16(uint8_t* p, const F128& v) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u d = {v.w[0], v.w[1], v.w[2], v.w[3]};
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)p;
+  asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(d) : "memory");
+}
+
 // Two in-place radix-2 DIT NTTs of size m (inputs already bit-reversed) over LDS arrays A and B,
 // twiddles in Montgomery form:  X[k] = sum_i x[i] alpha_m^(ik).
 template <class FO>
@@ -1325,8 +1334,13 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   bool bad = false;
   // block-start prefix products, element-major: entry b holds P_(8b) of report rr
   auto S = [&](uint32_t b) { return scr + ((size_t)b * n + rr) * 16u; };
-  // this lane's slot u of a window
-  auto put = [&](uint8_t* w, uint32_t u, const T& v) { FO::store(w + 128u * lane + 16u * (u ^ sw), v); };
+  // this lane's slot u of a window.  An inline-asm ds_write: hipcc cannot tell a plain LDS store
+  // from a write the earlier LDS-DMA fills might race with, and put a vmcnt(0) in front of every
+  // one -- a wait for the flush's global stores (the fills themselves are waited for explicitly
+  // before the window is read, and are all done before the backward pass writes win)
+  auto put = [&](uint8_t* w, uint32_t u, const T& v) {
+    lds_store16(w + 128u * lane + 16u * (u ^ sw), v);
+  };
   // gadget-poly window <- coefficients [8 ch, 8 ch + 8) of the wave's 64 rows (LDS-DMA instruction
   // i fills slots [64i, 64i + 64): report 8i + lane/8, element (lane & 7) ^ swizzle)
   auto stage = [&](uint32_t ch) {
