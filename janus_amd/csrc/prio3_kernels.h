@@ -1389,8 +1389,8 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   for (uint32_t k = 1; k <= steps; ++k) {
     if (k <= C && ((k - 1u) & 7u) == 0u) FO::store(S((k - 1u) >> 3), P);
     const T d = FO::sub(tm, ld_tw<FO>(cfg, k <= C ? k : 1u));
-    T nP, nrp, idle;
-    mul3<FO>(P, d, rp, rm, one, one, nP, nrp, idle);
+    T nP, nrp;
+    mont_mul2(P, d, nP, rp, rm, nrp);
     if (k <= C) P = nP;
     if (k <= c) {
       rp = nrp;
@@ -1472,6 +1472,14 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
     for (uint32_t u = 1; u < kFwChunk; ++u)
       if (u < nb) pb[u] = FO::mul(pb[u - 1], FO::sub(tm, ld_tw<FO>(cfg, lo + u - 1u)));
     T ptw = one;
+    // MM of an entry (L_k q) is formed one step later, beside the next entry's chain products,
+    // so every step issues five independent products (mont_mul5)
+    T lkp = FO::zero(), qp = FO::zero();
+    auto emit_mm = [&](uint32_t u, const T& mm_raw) {
+      const T mm = rz ? (lo + u == 1u ? lkp : FO::zero()) : mm_raw;
+      put(win, u, mm);
+      smm = FO::add(smm, mm);
+    };
 #pragma unroll
     for (int u = kFwChunk - 1; u >= 0; --u) {
       if ((uint32_t)u < nb) {
@@ -1480,21 +1488,21 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
         const T d = FO::sub(tm, ld_tw<FO>(cfg, k));
         const T pn = u > 0 ? pb[u > 0 ? u - 1 : 0] : one;
         const T tn = u > 0 ? ld_tw<FO>(cfg, 2u * m + k) : one;
-        T lk, ninv, nptw;
-        // the chain step {inv pt_k, inv d_k} and the next entry's P_(k-2) alpha^(k-1)/m
-        mul3<FO>(inv, ptw, inv, d, pn, tn, lk, ninv, nptw);
+        // the chain step {inv pt_k, inv d_k}, the next entry's P_(k-2) alpha^(k-1)/m,
+        // q <- q / r^c, and MM of the previous entry (k + 1)
+        T lk, ninv, nptw, nq, mmp;
+        mont_mul5(inv, ptw, lk, inv, d, ninv, pn, tn, nptw, q, rcinv, nq, lkp, qp, mmp);
+        if ((uint32_t)u + 1u < nb) emit_mm((uint32_t)u + 1u, mmp);
         inv = ninv;
         ptw = nptw;
-        T mm, nq, idle;
-        mul3<FO>(lk, q, q, rcinv, one, one, mm, nq, idle);
-        if (rz) mm = k == 1u ? lk : FO::zero();
+        lkp = lk;
+        qp = q;
         q = nq;
         put(wout, (uint32_t)u, lk);
-        put(win, (uint32_t)u, mm);
         lsum = FO::add(lsum, lk);
-        smm = FO::add(smm, mm);
       }
     }
+    emit_mm(0u, FO::mul(lkp, qp));
     flush(wout, W.lm(lo - 1u), nb);
     flush(win, W.mm(lo - 1u), nb);
   }

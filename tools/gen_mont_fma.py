@@ -528,6 +528,10 @@ FUNCTIONS = {
     "mont_fma3_mul1": ["F", "F", "F", "M"],
     #   then the gadget-output fraction's numerator + the wire fraction (numerator, denominator)
     "mont_fma2_mul1": ["F", "F", "M"],
+    # k_flp_weights: the forward pass (prefix product + r^j), the backward pass (L_k, the inverse
+    # and weight chains, q <- q / r^c and the previous entry's MM), Horner in t^3
+    "mont_mul2": ["M", "M"],
+    "mont_mul5": ["M", "M", "M", "M", "M"],
 }
 
 
