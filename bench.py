@@ -119,6 +119,21 @@ def flp_wires_bytes_per_report(s, mfma=False):
     return (s.meas_len + w_len + 2 * arity) * es
 
 
+def flp_weights_bytes_per_report(s):
+    """Algorithmic HBM bytes of k_flp_weights per report (ParallelSum types): the
+    gadget-poly part of the proof share and t, r read; the weight row MM[calls] | LM[calls] |
+    RP[c] | L0 | HL | gsum | SMM | SLM written; the block-start prefix products (one per 8 calls)
+    written and read back; v, p(t) and the 16-byte part copied into the prep share."""
+    es = s.field_size
+    arity = s.verifier_len - 2
+    c = arity // 2
+    calls = -(-s.meas_len // c)
+    gp_len = s.proof_len - arity
+    w_len = 2 * calls + c + 5
+    scratch = 2 * ((calls + 7) // 8)
+    return (gp_len + 2 + w_len + scratch + 2) * es + 2 * 16
+
+
 def flp_mults_per_report(sizes, kind):
     """SURVEY §8(d)'s FLP op model: field multiplications of ONE aggregator's prio-style FLP query
     (Type::query with the QueryShim gadget; count the spec algorithm, not this engine's): every
@@ -823,6 +838,20 @@ def main():
             hb["traffic"] = hp["hbm_bytes_per_launch"]
             hb["traffic_over_algorithmic"] = round(hp["hbm_bytes_per_launch"] / alg, 3)
         roof["hbm"] = hb
+    # the weights kernel beside it: its HBM line, PMC traffic per launch
+    if kt.get("k_flp_weights", (0, 0))[1]:
+        wms, wl = kt["k_flp_weights"]
+        w_avg = wms / 1e3 / wl
+        walg = nlaunch * flp_weights_bytes_per_report(s)
+        wline = {"kernel": "k_flp_weights", "avg_launch_ms": round(w_avg * 1e3, 3),
+                 "algorithmic_bytes_per_launch": walg,
+                 "achieved": round(walg / w_avg / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(walg / w_avg / 1e9 / HBM_PEAK_GBS, 4), "traffic": None}
+        wp = pmc.get("kernels", {}).get("k_flp_weights")
+        if wp and wp.get("hbm_bytes_per_launch"):
+            wline["traffic"] = wp["hbm_bytes_per_launch"]
+            wline["traffic_over_algorithmic"] = round(wp["hbm_bytes_per_launch"] / walg, 3)
+        roof["hbm_weights"] = wline
 
     # ---- CPU baseline: C restatement of prio 0.15.1, bounded sample, rank 0 at N = 1 -----------
     cpu = None

@@ -294,12 +294,35 @@ DEVI void derive_jr_seed(const Xof& x, uint32_t algo_id, uint64_t p0lo, uint64_t
 // Message = 42-byte prefix || data (nbytes, multiple of 8) || SHAKE padding.  Stream word g >= 5 is
 // (D[g-6] >> 48) | (D[g-5] << 16) with D[-1] = the top 16 bits of the nonce's high word.
 // ------------------------------------------------------------------------------------------------
-// word g >= 5 of the stream:  (D[i-1] >> 48) | (D[i] << 16),  i = g - 5,  D[-1] = nonce_hi
-DEVI uint64_t jr_data_word(int64_t g, const uint8_t* data, int64_t nd, uint64_t nonce_hi) {
-  const int64_t i = g - 5;
-  uint64_t lo = (i == 0) ? (nonce_hi >> 48) : ((i - 1 < nd) ? (ld64(data + 8 * (i - 1)) >> 48) : 0ull);
-  uint64_t hi = (i < nd) ? (ld64(data + 8 * i) << 16) : 0ull;
-  return lo | hi;
+// Words 21b .. 21b+20 of block b (b >= 0; words < 5 of block 0 are the caller's prefix), cut from
+// the 22 data words D[21b-6 .. 21b+15]: loaded in two batches of 11 from clamped addresses (one
+// wait per batch instead of a load-use wait per word), selected, funnel-shifted and handed to
+// emit(w, word) as soon as formed, so at most one batch is live (k_jr stays within 168 VGPRs).
+template <class Emit>
+DEVI void jr_block_words(int64_t b, const uint8_t* data, int64_t nd, uint64_t nonce_hi,
+                         Emit&& emit) {
+  const int64_t j0 = 21 * b - 6;
+  auto ld = [&](int k) {
+    const int64_t j = j0 + k;
+    return ld64(data + 8 * (j < 0 ? 0 : (j < nd ? j : nd - 1)));
+  };
+  auto fix = [&](int k, uint64_t d) {
+    const int64_t j = j0 + k;
+    return (j >= 0 && j < nd) ? d : (j == -1 ? nonce_hi : 0ull);
+  };
+  uint64_t D[11];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) D[k] = ld(k);
+#pragma unroll
+  for (int w = 0; w < 10; ++w) emit(w, (fix(w, D[w]) >> 48) | (fix(w + 1, D[w + 1]) << 16));
+  const uint64_t d10 = fix(10, D[10]);
+  asm volatile("" ::: "memory");  // the second batch is not hoisted above the first one's use
+#pragma unroll
+  for (int k = 0; k < 11; ++k) D[k] = ld(11 + k);
+  emit(10, (d10 >> 48) | (fix(11, D[0]) << 16));
+#pragma unroll
+  for (int w = 11; w < 21; ++w)
+    emit(w, (fix(w, D[w - 11]) >> 48) | (fix(w + 1, D[w - 10]) << 16));
 }
 
 DEVI void jr_part(const Xof& x, uint32_t algo_id, uint32_t agg_id, uint64_t blind_lo, uint64_t blind_hi,
@@ -335,21 +358,21 @@ DEVI void jr_part(const Xof& x, uint32_t algo_id, uint32_t agg_id, uint64_t blin
       }
     } else if (b == 0) {
 #pragma unroll
-      for (int w = 0; w < 21; ++w) {
-        uint64_t v = (w < 5) ? pre.w[w] : jr_data_word(w, data, nd, nonce_hi);
+      for (int w = 0; w < 5; ++w) s[w] ^= (padw == w) ? pre.w[w] ^ padv : pre.w[w];
+      asm volatile("" ::: "memory");  // the prefix is absorbed before the data words load
+      jr_block_words(0, data, nd, nonce_hi, [&](int w, uint64_t v) {
+        if (w < 5) return;
         if (padw == w) v ^= padv;
         if (nblocks == 1 && w == 20) v ^= 0x8000000000000000ull;
         s[w] ^= v;
-      }
+      });
     } else {
-#pragma unroll
-      for (int w = 0; w < 21; ++w) {
+      jr_block_words(b, data, nd, nonce_hi, [&](int w, uint64_t v) {
         const int64_t g = 21 * b + w;
-        uint64_t v = jr_data_word(g, data, nd, nonce_hi);
         if (padw == g) v ^= padv;
         if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
         s[w] ^= v;
-      }
+      });
     }
     keccak_x(s, x);
   }
@@ -434,7 +457,7 @@ constexpr uint32_t kJrWin = 176;  // bytes per report in the LDS window (22 word
 constexpr uint32_t kJrWaveLds = 64 * kJrWin;
 
 template <class FO>
-__global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id, CRows nonces,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id, CRows nonces,
                                             CRows public_shares, CRows blinds, CRows meas,
                                             Rows out_part, Rows out_seed, Rows out_jr,
                                             const uint8_t* status, uint64_t* spec_lo,
@@ -585,21 +608,21 @@ __global__ void __launch_bounds__(256) k_jr(Cfg cfg, uint32_t n, uint32_t agg_id
       pre.put64(26, ld64(nz));
       pre.put64(34, nonce_hi);
 #pragma unroll
-      for (int w = 0; w < 21; ++w) {
-        uint64_t v = (w < 5) ? pre.w[w] : jr_data_word(w, data, nd, nonce_hi);
+      for (int w = 0; w < 5; ++w) s[w] ^= (padw == w) ? pre.w[w] ^ padv : pre.w[w];
+      asm volatile("" ::: "memory");  // the prefix is absorbed before the data words load
+      jr_block_words(0, data, nd, nonce_hi, [&](int w, uint64_t v) {
+        if (w < 5) return;
         if (padw == w) v ^= padv;
         if (nblocks == 1 && w == 20) v ^= 0x8000000000000000ull;
         s[w] ^= v;
-      }
+      });
     } else {
-#pragma unroll
-      for (int w = 0; w < 21; ++w) {
-        const int64_t g = 21 * b + w;  // >= 21: the nonce word is never needed here
-        uint64_t v = jr_data_word(g, data, nd, 0ull);
+      jr_block_words(b, data, nd, 0ull, [&](int w, uint64_t v) {  // b >= 1: no nonce word
+        const int64_t g = 21 * b + w;
         if (padw == g) v ^= padv;
         if (b == nblocks - 1 && w == 20) v ^= 0x8000000000000000ull;
         s[w] ^= v;
-      }
+      });
     }
     if (is_fast(b + 1)) {  // refill the window (its reads above have completed) under the permutation
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -35,3 +35,14 @@ def test_flp_op_model_matches_survey_appendix_b():
     assert 4000 <= bench.flp_mults_per_report(mk(16, 256, 95, 34), 3) <= 4700
     assert 115000 <= bench.flp_mults_per_report(mk(16, 8000, 433, 180), 2) <= 130000
     assert bench.flp_mults_per_report(mk(8, 1, 5, 4), 0) == 14
+
+
+def test_flp_weights_bytes_model():
+    """k_flp_weights' algorithmic bytes per report (bench.py roofline.hbm_weights): SumVec(8,1000)
+    reads 255 gadget coefficients + t, r and writes a 274-entry weight row, 12 block-start prefix
+    products (written and read back), v, p(t) and the 16-byte part copy."""
+    import bench
+    from types import SimpleNamespace as NS
+    s = NS(field_size=16, meas_len=8000, proof_len=433, verifier_len=180)
+    assert bench.flp_weights_bytes_per_report(s) == (255 + 2 + 274 + 24 + 2) * 16 + 32
+    assert 3.4e9 < 393216 * bench.flp_weights_bytes_per_report(s) < 3.6e9
