@@ -1065,15 +1065,15 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
   const T tm = FO::to_mont(FO::load(tq.at(rr)));
   T tmm = tm;
   // Sum: t^m, r^m and r^calls (calls < m, right-to-left square-and-multiply) advance together,
-  // one triple of squarings per bit
+  // one triple per bit: t and r squared, r^calls times r^(2^q) (or times one)
   T rm = FO::zero(), rmm = FO::zero(), rc = one, th = tm;
   if (cfg.kind == KIND_SUM) {
     rm = FO::to_mont(FO::load(jr.at(rr)));
     rmm = rm;
-    T b = rm;
-    for (uint32_t q = 0; q < cfg.logm; ++q) {
-      if ((calls >> q) & 1u) rc = FO::mul(rc, b);
-      mul3<FO>(tmm, tmm, rmm, rmm, b, b, tmm, rmm, b);
+    for (uint32_t q = 0; q < cfg.logm; ++q) {  // rmm = r^(2^q) before the step
+      T nrc;
+      mul3<FO>(tmm, tmm, rmm, rmm, rc, ((calls >> q) & 1u) ? rmm : one, tmm, rmm, nrc);
+      rc = nrc;
       if (q + 2u == cfg.logm) th = tmm;  // t^(m/2)
     }
   } else {

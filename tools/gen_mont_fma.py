@@ -31,7 +31,7 @@ R = 1 << 128
 # ---------------------------------------------------------------------------------------------
 # programs of one operation (register names local to the operation, prefix added later)
 # ---------------------------------------------------------------------------------------------
-def product(fused):
+def product(fused, rename=False):
     """Column sums of a b (+ c d): L0..L6 (64-bit), carries h0..h6 (32-bit; h_c sits at
     2^(32 c + 64)).  Each mad's carry is read by the addc right after it (the interleave or the
     emitter's s_nop gives the wait states)."""
@@ -48,9 +48,10 @@ def product(fused):
                     first.add(c)
                     ins.append(("mad", f"L{c}", "cd", f"{x}{i}", f"{y}{j}", 0))
                 else:
-                    ins.append(("mad", f"L{c}", "cy", f"{x}{i}", f"{y}{j}", f"L{c}"))
+                    cy = f"cy{c}" if rename else "cy"  # per-column carries let columns interleave
+                    ins.append(("mad", f"L{c}", cy, f"{x}{i}", f"{y}{j}", f"L{c}"))
                     # the first carry into h_c sets it (h_c = 0 + 0 + carry), later ones add
-                    ins.append(("addc", f"h{c}", "cd", f"h{c}" if c in hset else 0, 0, "cy"))
+                    ins.append(("addc", f"h{c}", "cd", f"h{c}" if c in hset else 0, 0, cy))
                     hset.add(c)
     return ins
 
@@ -248,6 +249,157 @@ def interleave(streams):
     return out
 
 
+def rw_sets(ins):
+    """(registers read, registers written) of one instruction; the carry dump "cd" and the
+    constant P2 carry no dependencies."""
+    op = ins[0]
+    if op == "mad":
+        R, W = [ins[3], ins[4], ins[5]], [ins[1], ins[2]]
+    elif op in ("add_co", "sub_co"):
+        R, W = [ins[3], ins[4]], [ins[1], ins[2]]
+    elif op in ("addc", "subb"):
+        R, W = [ins[3], ins[4], ins[5]], [ins[1], ins[2]]
+    elif op in ("lsl", "lsr"):
+        R, W = [ins[3]], [ins[1]]
+    elif op == "abit":
+        R, W = [ins[2], ins[3]], [ins[1]]
+    elif op == "cnd":
+        R, W = [ins[2], ins[3], ins[4]], [ins[1]]
+    elif op in ("vsub", "and"):
+        R, W = [ins[2], ins[3]], [ins[1]]
+    else:
+        raise ValueError(op)
+    R = [r for r in R if isinstance(r, str) and r not in ("P2", "cd")]
+    W = [x for x in W if x != "cd"]
+    return R, W
+
+
+def carry_reads(ins):
+    op = ins[0]
+    return [ins[5]] if op in ("addc", "subb") else [ins[4]] if op == "cnd" else []
+
+
+def list_schedule(streams):
+    """streams: lists of (ins, stream_id), independent of each other.  Greedy list scheduling in
+    round-robin priority: each slot issues the first instruction whose predecessors (RAW, WAR,
+    WAW within its stream) have issued and whose carry inputs were written >= WAIT + 1 slots
+    earlier; s_nop only when nothing is ready.  Same output form as interleave()."""
+    order, pos = [], [0] * len(streams)
+    while any(p < len(st) for p, st in zip(pos, streams)):
+        for k, st in enumerate(streams):
+            if pos[k] < len(st):
+                order.append(st[pos[k]])
+                pos[k] += 1
+    n = len(order)
+    deps = [[] for _ in range(n)]
+    last_w, readers = {}, {}
+    for i, (ins, sid) in enumerate(order):
+        R, W = rw_sets(ins)
+        cr = set(carry_reads(ins))
+        for r in R:
+            if (sid, r) in last_w:
+                deps[i].append((last_w[(sid, r)], WAIT + 1 if r in cr else 1))
+        for x in W:
+            if (sid, x) in last_w:
+                deps[i].append((last_w[(sid, x)], 1))
+            deps[i] += [(j, 1) for j in readers.get((sid, x), []) if j != i]
+        for r in R:
+            readers.setdefault((sid, r), []).append(i)
+        for x in W:
+            last_w[(sid, x)] = i
+            readers[(sid, x)] = []
+    at = [None] * n
+    out, slot, left = [], 0, list(range(n))
+    while left:
+        pick, wait = None, None
+        for i in left:
+            need, ok = 0, True
+            for j, d in deps[i]:
+                if at[j] is None:
+                    ok = False
+                    break
+                need = max(need, at[j] + d - slot)
+            if not ok:
+                continue
+            if need <= 0:
+                pick = i
+                break
+            wait = need if wait is None else min(wait, need)
+        if pick is None:
+            out.append((("nop", wait - 1), None))
+            slot += wait
+            continue
+        at[pick] = slot
+        out.append(order[pick])
+        left.remove(pick)
+        slot += 1
+    return out
+
+
+def qualify(ins, sid):
+    """register names of one instruction prefixed with its stream (the opcode and P2 kept)"""
+    return (ins[0],) + tuple(f"{sid}.{x}" if isinstance(x, str) and x != "P2" else x
+                             for x in ins[1:])
+
+
+def check_schedule(sched, init, expect):
+    """Run a scheduled stream (registers qualified by stream) on the simulator and check every
+    carry read's distance to its write: init = {(sid, reg): value}, expect = {(sid, reg): value}."""
+    st = {f"{sid}.{r}": v for (sid, r), v in init.items()}
+    last, slot = {}, 0
+    for ins, sid in sched:
+        if ins[0] == "nop":
+            slot += ins[1] + 1
+            continue
+        q = qualify(ins, sid)
+        for r in carry_reads(ins):
+            assert slot - last[(sid, r)] >= WAIT + 1, ("carry hazard", ins, sid)
+        simulate([q], st)
+        if ins[0] in CARRY_OPS:
+            last[(sid, ins[CARRY_OPS[ins[0]]])] = slot
+        slot += 1
+    for (sid, r), v in expect.items():
+        assert st[f"{sid}.{r}"] == v, ("schedule result", sid, r)
+
+
+def verify_function(ops, progs, sched, rsched, trials=40):
+    """The scheduled product and reduction streams of one generated function against Python
+    integers, on random and edge operands, with the carry-hazard check of check_schedule."""
+    rng = random.Random(len(sched) * 7 + len(rsched))
+    edge = [0, 1, P - 1, P - 2, (1 << 128) - 28 * (1 << 64)]
+    rinv = pow(R, -1, P)
+    for t in range(trials):
+        init, want, mid = {}, {}, {}
+        for s, q, fused, tag in ops:
+            vals = [rng.choice(edge) if (t + k) % 5 == 0 else rng.randrange(P) for k in range(4)]
+            for i in range(4):
+                for nm, v in zip("abcd", vals):
+                    init[(tag, f"{nm}{i}")] = (v >> (32 * i)) & M32
+            for c in range(7):
+                init[(tag, f"h{c}")] = 0xDEADBEEF
+            for h in product_inits(fused):
+                init[(tag, h)] = 0
+            a, b, c_, d = vals
+            want[tag] = (a * b + (c_ * d if fused else 0)) * rinv % P
+        st = {f"{sid}.{r}": v for (sid, r), v in init.items()}
+        check_schedule(sched, init, {})
+        # rerun to read the product state, split L into halves for the reduction
+        for ins, sid in sched:
+            if ins[0] != "nop":
+                simulate([qualify(ins, sid)], st)
+        rin = {}
+        for s, q, fused, tag in ops:
+            for c in range(7):
+                Lc = st[f"{tag}.L{c}"]
+                rin[(tag, f"l{c}")], rin[(tag, f"g{c}")] = Lc & M32, Lc >> 32
+                rin[(tag, f"h{c}")] = st[f"{tag}.h{c}"]
+        exp = {}
+        for s, q, fused, tag in ops:
+            for i in range(4):
+                exp[(tag, f"r{i}")] = (want[tag] >> (32 * i)) & M32
+        check_schedule(rsched, rin, exp)
+
+
 def gen_function(name, spec, volatile=True):
     """spec: one string per stream of "F" (fused) / "M" (single) operations, e.g. ["F", "F", "MM"].
     Signature: for every operation in stream order, (a, b[, c, d]) inputs then its output."""
@@ -273,12 +425,16 @@ def gen_function(name, spec, volatile=True):
         ops_e.append(expr)
         cons.append(con)
 
+    rename = len(ops) <= 2  # per-column carries (7 SGPR pairs per product) for 1-2 products
+    progs = {tag: product(fused, rename) for s, q, fused, tag in ops}
+    carries = {tag: sorted({i[2] for i in pr if i[0] == "mad" and i[2] != "cd"})
+               for tag, pr in progs.items()}
     for s, q, fused, tag in ops:
         w(f"  uint64_t L{tag}[7];")
         w(f"  uint32_t h{tag}[7];")
         for h in product_inits(fused):
             w(f"  h{tag}[{h[1:]}] = 0u;")
-        w(f"  uint64_t cy{tag};")
+        w(f"  uint64_t " + ", ".join(f"{cy}_{tag}" for cy in carries[tag]) + ";")
     w("  uint64_t cdump;")
     for s, q, fused, tag in ops:
         for c in range(7):
@@ -286,7 +442,8 @@ def gen_function(name, spec, volatile=True):
         zero = product_inits(fused)
         for c in range(7):
             opnd(f"h{c}_{tag}", '"+v"' if f"h{c}" in zero else '"=&v"', f"h{tag}[{c}]")
-        opnd(f"cy_{tag}", '"=&s"', f"cy{tag}")
+        for cy in carries[tag]:
+            opnd(f"{cy}_{tag}", '"=&s"', f"{cy}_{tag}")
     opnd("cd", '"=&s"', "cdump")
     nout = len(ops_e)
     for s, q, fused, tag in ops:
@@ -304,9 +461,12 @@ def gen_function(name, spec, volatile=True):
             return f"%{idx['cd']}"
         return f"%{idx[f'{x}_{tag}']}"
 
-    # every operation is its own stream (they are independent), so the round-robin spacing grows
-    # with the number of operations and unequal lengths leave only short unpaired tails
-    sched = interleave([[(ins, tag) for ins in product(fused)] for (ss, q, fused, tag) in ops])
+    # every operation is its own stream (they are independent); list-scheduled, then re-run on
+    # the simulator and hazard-checked (verify_function)
+    sched = list_schedule([[(ins, tag) for ins in progs[tag]] for (ss, q, fused, tag) in ops])
+    rsched = list_schedule([[(ins, tag) for ins in aliased(reduce_program(fused))]
+                            for (ss, q, fused, tag) in ops])
+    verify_function(ops, progs, sched, rsched)
     lines = []
     for ins, tag in sched:
         if ins[0] == "nop":
@@ -352,8 +512,7 @@ def gen_function(name, spec, volatile=True):
             return f"%{idx['P2']}"
         return f"%{idx[f'{x}_{tag}']}"
 
-    sched = interleave([[(ins, tag) for ins in aliased(reduce_program(fused))]
-                        for (ss, q, fused, tag) in ops])
+    sched = rsched
     mn = {"add_co": "v_add_co_u32_e64", "addc": "v_addc_co_u32_e64", "sub_co": "v_sub_co_u32_e64",
           "subb": "v_subb_co_u32_e64"}
     lines = []
@@ -382,7 +541,7 @@ def gen_function(name, spec, volatile=True):
     w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[nout:], ops_e[nout:])) + ");")
     w("}")
     w("")
-    nops = sum(1 for l in lines if l.startswith("s_nop"))
+    nops = sum(int(l.split()[1]) + 1 for l in lines if l.startswith("s_nop"))
     return "\n".join(out), nops
 
 
@@ -396,11 +555,12 @@ def modadd_program():
     for i in range(1, 4):
         ins.append(("addc", f"r{i}", "k", f"a{i}", f"b{i}", "k"))
     ins.append(("addc", "q", "k", 0, 0, "k"))  # q = k1
-    ins.append(("add_co", "x", "k", "r0", -1))
-    ins.append(("addc", "x", "k", "r1", -1, "k"))
-    ins.append(("addc", "x", "k", "r2", 27, "k"))
-    ins.append(("addc", "x", "k", "r3", 0, "k"))
-    ins.append(("addc", "q", "k", "q", 0, "k"))  # q = k1 + k2
+    # the detect chain has its own carry, so it can start as soon as r0 is formed
+    ins.append(("add_co", "x", "k2", "r0", -1))
+    ins.append(("addc", "x", "k2", "r1", -1, "k2"))
+    ins.append(("addc", "x", "k2", "r2", 27, "k2"))
+    ins.append(("addc", "x", "k2", "r3", 0, "k2"))
+    ins.append(("addc", "q", "k2", "q", 0, "k2"))  # q = k1 + k2
     ins.append(("vsub", "m", 0, "q"))
     ins.append(("and", "x", 27, "m"))
     ins.append(("add_co", "r0", "k", "r0", "m"))
@@ -468,7 +628,7 @@ def gen_addsub(name, spec, volatile=True):
 
     for q, kind, tag in ops:
         w(f"  uint32_t x{tag}, m{tag}" + (f", q{tag};" if kind == "A" else ";"))
-        w(f"  uint64_t k{tag};")
+        w(f"  uint64_t k{tag}" + (f", kk{tag};" if kind == "A" else ";"))
     for q, kind, tag in ops:
         for i in range(4):
             opnd(f"r{i}_{tag}", '"=&v"', f"r{tag}.w[{i}]")
@@ -476,6 +636,7 @@ def gen_addsub(name, spec, volatile=True):
         opnd(f"m_{tag}", '"=&v"', f"m{tag}")
         if kind == "A":
             opnd(f"q_{tag}", '"=&v"', f"q{tag}")
+            opnd(f"k2_{tag}", '"=&s"', f"kk{tag}")
         opnd(f"k_{tag}", '"=&s"', f"k{tag}")
     nout = len(ops_e)
     for q, kind, tag in ops:
@@ -488,10 +649,22 @@ def gen_addsub(name, spec, volatile=True):
 
     progs = [[(ins, tag) for ins in (modadd_program() if kind == "A" else modsub_program())]
              for (q, kind, tag) in ops]
+    sched = list_schedule(progs)
+    rng = random.Random(len(spec))
+    for t in range(200):
+        init, exp = {}, {}
+        for q, kind, tag in ops:
+            a, b = rng.randrange(P), rng.randrange(P)
+            if t % 7 == 0:
+                a, b = P - 1, P - 1 - (t % 3)
+            for i in range(4):
+                init[(tag, f"a{i}")], init[(tag, f"b{i}")] = (a >> 32 * i) & M32, (b >> 32 * i) & M32
+                exp[(tag, f"r{i}")] = (((a + b) if kind == "A" else (a - b)) % P >> 32 * i) & M32
+        check_schedule(sched, init, exp)
     mn = {"add_co": "v_add_co_u32_e64", "addc": "v_addc_co_u32_e64", "sub_co": "v_sub_co_u32_e64",
           "subb": "v_subb_co_u32_e64"}
     lines = []
-    for ins, tag in interleave(progs):
+    for ins, tag in sched:
         op = ins[0]
         if op == "nop":
             lines.append(f"s_nop {ins[1]}")
@@ -510,7 +683,7 @@ def gen_addsub(name, spec, volatile=True):
     w("      : " + ", ".join(f"{c}({e})" for c, e in zip(cons[nout:], ops_e[nout:])) + ");")
     w("}")
     w("")
-    nops = sum(1 for l in lines if l.startswith("s_nop"))
+    nops = sum(int(l.split()[1]) + 1 for l in lines if l.startswith("s_nop"))
     return "\n".join(out), nops
 
 
