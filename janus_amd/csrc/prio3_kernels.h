@@ -904,7 +904,7 @@ DEVI typename FO::T inv_mont(const typename FO::T& x) {
   else return inv_mont64(x);
 }
 
-// Sum's FLP query when calls = m/2 (power-of-two bits, m >= 4) and r^m != 1, Field128, one lane
+// Sum's FLP query when calls = m/2 (power-of-two bits, m >= 8) and r^m != 1, Field128, one lane
 // per report: the same field values as the generic loop below, from fewer products.  With
 // h = m/2 = calls, alpha^h = -1, beta_i = alpha^-i (tables, Montgomery):
 //   * gadget-output sum  v = sum_i F_i G(y_i),  F_i = c_i + c_(i+m),  y_i = r alpha^i,
@@ -923,15 +923,18 @@ DEVI typename FO::T inv_mont(const typename FO::T& x) {
 // advanced by a product) and 8 + 16 products of the mul3 loop.
 // Domains: values marked M are Montgomery form (x R), the rest plain; mont(M, plain) is plain.
 // Operands: iteration i reads c_i, c_(i+m), c_(i+h), c_(i+h+m) (gadget coefficients, proof
-// elements 1 + .) and x_i (measurement element i - 1; x_0 = the proof seed).  A loop trip (odd i,
-// then i - 1) takes two consecutive elements of each of these five streams, which arrive by LDS-DMA
-// into a per-wave window of 5 x 2 KB (kSqWin): instruction k of a stream fills 1 KB = 32 reports x
-// 2 elements, slot 2q + (u ^ ((q >> 2) & 1)) holding element u of report q (each lane's
-// ds_read_b128 of its own report is then bank-conflict-free).  The next trip's DMA is issued once
-// the second iteration's operands sit in registers, so it lands under that iteration's products
-// and no VGPRs are held by loads in flight.  Every lane of the wave takes part (dead lanes compute
-// on a clamped row).
-constexpr uint32_t kSqWin = 5u * 2048u;  // bytes per wave
+// elements 1 + .) and x_i (measurement element i - 1; x_0 = the proof seed).  A loop trip (i0 + 3
+// down to i0, i0 = 0 mod 4) takes four consecutive elements (64 B) of each of these five streams,
+// which arrive by LDS-DMA into a per-wave window of 5 x 4 KB (kSqWin): instruction k of a stream
+// fills 1 KB = 16 reports x 4 elements, slot 4q + (u ^ ((q >> 1) & 3)) holding element u of report
+// q (each lane's ds_read_b128 of its own report is then bank-conflict-free).  The next trip's DMA
+// is issued once the trip's last operands sit in registers, so it lands under that iteration's
+// products; no VGPRs are held by loads in flight.  64-B runs per report (rather than 32) halve the
+// HBM sectors fetched per byte used (PMC: 12.4 GB per 1M-report launch with 2-element windows
+// against 2.6 GB of operands).  Every lane of the wave takes part (dead lanes compute on a clamped
+// row).
+constexpr uint32_t kSqEl = 4u;                      // elements per stream per trip
+constexpr uint32_t kSqWin = 5u * 64u * 16u * kSqEl;  // bytes per wave (20 KB)
 
 DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane, CRows meas,
                          CRows proof, uint8_t* win, const F128& tm, const F128& th,
@@ -943,14 +946,15 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
   const T one = FO::one_mont();
   const T t3h = FO::mul(tmm, th);                    // M(t^(m + h))
   const T r2 = FO::mul(rm, rm);                      // M(r^2)
-  // DMA of the trip whose first (odd) iteration is i: elements i - 1, i of the five streams
-  auto stage = [&](uint32_t i) {
+  constexpr uint32_t SB = 64u * 16u * kSqEl;          // bytes per stream window
+  // DMA of the trip covering elements i0 .. i0 + 3 of the five streams
+  auto stage = [&](uint32_t i0) {
     uint32_t ln;  // opaque copy: the row addresses are recomputed per trip, never held
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-    const uint32_t e = i - 1u + ((ln & 1u) ^ ((ln >> 3) & 1u));  // this lane's element
+    const uint32_t e = i0 + ((ln & 3u) ^ ((ln >> 3) & 3u));  // this lane's element
 #pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) {
-      const uint32_t row = min(r0w + 32u * k + (ln >> 1), n - 1u);
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t row = min(r0w + 16u * k + (ln >> 2), n - 1u);
       const uint8_t* pr = proof.base + (size_t)row * proof.stride;
       const uint8_t* xr = meas.base + (size_t)row * meas.stride;
       const uint32_t off[4] = {e, e + m, e + h, (uint32_t)min(e + h + m, gp_len - 1u)};
@@ -958,14 +962,14 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
       for (uint32_t s = 0; s < 4; ++s)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(pr + 16u * (1u + off[s])),
-            (__attribute__((address_space(3))) void*)(win + 2048u * s + 1024u * k), 16, 0, 0);
+            (__attribute__((address_space(3))) void*)(win + SB * s + 1024u * k), 16, 0, 0);
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(xr + 16u * (e ? e - 1u : 0u)),
-          (__attribute__((address_space(3))) void*)(win + 2048u * 4u + 1024u * k), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(win + SB * 4u + 1024u * k), 16, 0, 0);
     }
   };
-  const uint32_t sl = 32u * lane, sw = (lane >> 2) & 1u;
-  auto rd = [&](uint32_t s, uint32_t u) { return FO::load(win + 2048u * s + sl + 16u * (u ^ sw)); };
+  const uint32_t sl = 64u * lane, sw = (lane >> 1) & 3u;
+  auto rd = [&](uint32_t s, uint32_t u) { return FO::load(win + SB * s + sl + 16u * (u ^ sw)); };
   T N[2] = {FO::zero(), FO::zero()};                 // gadget-output fractions by parity, plain
   T D[2] = {one, one};                               // their denominators, M
   T X = FO::load(meas.at(min(r0w + lane, n - 1u)) + (size_t)(h - 1) * 16);  // x_calls
@@ -973,16 +977,17 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
   T Nw = X, Dw = FO::sub(tm, ld_tw<FO>(cfg, h));     // plain / M(t - alpha^calls)
   // Horner's p_(i+1) = P1 + P2 + c_(i+1) is finished inside iteration i's additions
   T P1 = FO::zero(), P2 = FO::zero(), cprev = FO::zero();
-  stage(h - 1u);
+  stage(h - kSqEl);
   auto step = [&](uint32_t i, auto PAR) {
-    constexpr uint32_t par = decltype(PAR)::value;  // = i & 1 = the window slot
-    if (par) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this trip's window has landed
-    const T ci = rd(0, par), cim = rd(1, par), cj = rd(2, par);
-    const T cjm = i + h + m < gp_len ? rd(3, par) : FO::zero();
-    const T x = i ? rd(4, par) : s0;
-    if (!par && i) {  // operands of the trip in registers: the window is free for the next one
+    constexpr uint32_t par = decltype(PAR)::value;  // = i & 1
+    const uint32_t u = i & (kSqEl - 1u);               // window slot (wave-uniform)
+    if (u == kSqEl - 1u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the window landed
+    const T ci = rd(0, u), cim = rd(1, u), cj = rd(2, u);
+    const T cjm = i + h + m < gp_len ? rd(3, u) : FO::zero();
+    const T x = i ? rd(4, u) : s0;
+    if (u == 0u && i) {  // the trip's operands in registers: the window is free for the next one
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      stage(i - 1u);
+      stage(i - kSqEl);
     }
     bad |= !FO::is_canonical(ci) | !FO::is_canonical(cim) | !FO::is_canonical(cj) |
            !FO::is_canonical(cjm) | !FO::is_canonical(x);
@@ -1006,7 +1011,7 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
     X = Xn;
     cprev = ci;
   };
-  // h is even: the pairs (odd i, even i - 1) unroll with constant parity
+  // h = 0 mod 4: a window serves two loop bodies of (odd i, even i - 1), constant parities
   for (uint32_t i = h - 1;; i -= 2) {
     step(i, std::integral_constant<uint32_t, 1>{});
     step(i - 1, std::integral_constant<uint32_t, 0>{});
@@ -1035,8 +1040,8 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
   pt_out = pt;
 }
 
-#ifndef FLPQ_WAVES
-#define FLPQ_WAVES
+#ifndef FLPQ_WAVES  // at least 2 waves/SIMD (<= 256 VGPRs) for the Field128 paired Sum query
+#define FLPQ_WAVES __attribute__((amdgpu_waves_per_eu(2)))
 #endif
 template <class FO>
 __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint32_t n, CRows meas,
@@ -1050,7 +1055,7 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
   // LDS-DMA for all 64 lanes); every other shape: one independent lane per live report
   bool pair = false;
   if constexpr (FO::ES == 16)
-    pair = cfg.kind == KIND_SUM && 2u * cfg.calls == cfg.m && cfg.m >= 4u && cfg.arity == 1u;
+    pair = cfg.kind == KIND_SUM && 2u * cfg.calls == cfg.m && cfg.m >= 8u && cfg.arity == 1u;
   if (!pair && !live) return;
   const uint32_t lane = threadIdx.x & 63u, r0w = r - lane;
   if (pair && r0w >= n) return;  // wave-uniform

@@ -21,6 +21,10 @@ CONFIGS = {
     # bits not a power of two (calls != m / 2) and the extremes of the Sum query loop
     "sum5": dict(kind=1, ctor=lambda: O.Prio3.new_sum(5), bits=5, length=0, chunk=0),
     "sum1": dict(kind=1, ctor=lambda: O.Prio3.new_sum(1), bits=1, length=0, chunk=0),
+    # the paired Sum query's edges: m = 4 (generic loop), m = 8 (one 4-iteration window), m = 32
+    "sum2": dict(kind=1, ctor=lambda: O.Prio3.new_sum(2), bits=2, length=0, chunk=0),
+    "sum4": dict(kind=1, ctor=lambda: O.Prio3.new_sum(4), bits=4, length=0, chunk=0),
+    "sum16": dict(kind=1, ctor=lambda: O.Prio3.new_sum(16), bits=16, length=0, chunk=0),
     "sum64": dict(kind=1, ctor=lambda: O.Prio3.new_sum(64), bits=64, length=0, chunk=0),
     "sumvec_small": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(2, 10, 3), bits=2, length=10,
                          chunk=3),

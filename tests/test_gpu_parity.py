@@ -12,7 +12,8 @@ from tests.reports import CONFIGS, expected_aggregate, make_batch, plaintext_sum
 
 pytestmark = pytest.mark.gpu
 
-SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sum5": 24, "sum1": 16, "sum64": 16, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
+SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sum5": 24, "sum1": 16, "sum64": 16, "sum2": 70,
+         "sum4": 70, "sum16": 70, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
          "hist256": 24, "sumvec_8_1000": 6, "sumvec_odd_calls": 8, "sumvec_chunk128": 8, "sumvec_chunk65": 8, "fp16_3": 12, "fp32_5": 8, "fp64_4": 8, "fp16_300": 6,
          "fp16_5000": 2}
 FPVEC = [k for k in SIZES if k.startswith("fp")]
