@@ -439,10 +439,13 @@ __global__ void __launch_bounds__(256, P3G_EXPAND_WAVES) k_expand(Cfg cfg, uint3
 // instructions (global_load_lds_dwordx4, 16 B/lane, ~6 rows per instruction instead of 64) while
 // block b is permuted.  All lanes of a wave take part in the fill, so lanes past n or with a
 // failed status still run the loop (on a clamped row) and just do not store.
-// lo:hi += x (64-bit), cy += carry out
+// lo:hi += x (64-bit), cy += carry out.  s_nop 1: gfx950 wants two wait states between a VALU
+// that writes VCC and a VALU that reads it as carry-in (hipcc pads its own chains the same way).
 DEVI void acc_u64(uint32_t& lo, uint32_t& hi, uint32_t& cy, uint64_t x) {
   asm("v_add_co_u32 %0, vcc, %0, %3\n\t"
+      "s_nop 1\n\t"
       "v_addc_co_u32 %1, vcc, %1, %4, vcc\n\t"
+      "s_nop 1\n\t"
       "v_addc_co_u32 %2, vcc, 0, %2, vcc"
       : "+v"(lo), "+v"(hi), "+v"(cy)
       : "v"((uint32_t)x), "v"((uint32_t)(x >> 32))
