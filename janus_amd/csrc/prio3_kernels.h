@@ -1678,6 +1678,25 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
   }
 }
 
+// sum_q xs[q] 2^(32 q) mod p, the xs[q] being sums of < 2^32 32-bit words (canonical result)
+DEVI F128 f128_reduce_limb_sums(const uint64_t (&xs)[4]) {
+  typedef unsigned __int128 u128;
+  const u128 CC = ((u128)28u << 64) - 1u;  // 2^128 - p
+  const u128 P = ~(u128)0 - CC + 1u;
+  // exact value = lo + top 2^128
+  u128 acc = (u128)xs[0] + ((u128)xs[1] << 32);
+  u128 c64 = acc >> 64;
+  uint64_t w0 = (uint64_t)acc;
+  u128 hi = c64 + (u128)xs[2] + ((u128)xs[3] << 32);  // < 2^97
+  const u128 lo = ((u128)(uint64_t)hi << 64) | w0;
+  const uint64_t top = (uint64_t)(hi >> 64);
+  // 2^128 = CC (mod p): lo + top CC < 2^128 + 2^102, then at most one wrap and one subtraction
+  u128 v = lo + (u128)top * CC;
+  if (v < lo) v += CC;  // wrapped past 2^128 (v is tiny now)
+  if (v >= P) v -= P;
+  return F128{{(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96)}};
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_flp_wires for short rows (chunk <= 64, Field128: Histogram, small SumVec/CountVec): a group of
 // G = next_pow2(chunk) lanes per report, lane j = column j, every call k in that lane:
@@ -1705,20 +1724,35 @@ __global__ void __launch_bounds__(256) k_flp_wires_cols(Cfg cfg, uint32_t n, uin
   Wide wa, wb;
   wide_zero(wa);
   wide_zero(wb);
-  T xsum = FO::zero();
-  bool bad = false;
+  // Histogram's sum x: 32-bit limbs summed into 64-bit words, reduced once after the loop
+  uint64_t xs[4] = {0ull, 0ull, 0ull, 0ull};
+  // canonical check, one compare per element: only a word 2^32 - 1 on top can make x >= p; the
+  // exact test runs after the loop, over this lane's elements, only when some lane saw one
+  bool maybe = false;
   for (uint32_t k = 0; k < C; ++k) {
     const uint32_t idx = k * c + j;
     T x = FO::zero();
     if (col && idx < cfg.meas_len) {
       x = FO::load(xr + (size_t)idx * ES);
-      bad |= !FO::is_canonical(x);
+      maybe |= x.w[3] == 0xFFFFFFFFu;
     }
     const T mm = FO::load(wm.el(rr, k)), lm = FO::load(wm.el(rr, C + k));
     wide_mac(wa, mm, x);
     wide_mac(wb, lm, x);
-    if (cfg.kind == KIND_HISTOGRAM) xsum = FO::add(xsum, x);
+    if (cfg.kind == KIND_HISTOGRAM) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xs[q] += x.w[q];
+    }
   }
+  bool bad = false;
+  if (__ballot(maybe)) {  // rare (probability ~2^-32 per element): the exact test
+    for (uint32_t k = 0; k < C; ++k) {
+      const uint32_t idx = k * c + j;
+      if (col && idx < cfg.meas_len) bad |= !FO::is_canonical(FO::load(xr + (size_t)idx * ES));
+    }
+  }
+  T xsum = FO::zero();
+  if (cfg.kind == KIND_HISTOGRAM) xsum = f128_reduce_limb_sums(xs);
   const T a = wide_reduce(wa), b = wide_reduce(wb);
   uint8_t* outp = out_prep.at(rr);
   if (col) {

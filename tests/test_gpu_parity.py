@@ -152,7 +152,7 @@ def test_noncanonical_leader_share_is_invalid_message():
 
 
 @pytest.mark.parametrize("name", ["hist256", "sumvec_small", "countvec15", "sumvec_8_1000",
-                                  "sumvec_odd_calls"])
+                                  "sumvec_odd_calls", "sum8", "sum32"])
 def test_noncanonical_element_inside_a_lane_group(name):
     """A non-canonical measurement element deep inside the share (not the first element) rejects
     only its report, whichever lane of a multi-report wave (k_flp_wires_cols: G lanes per report)
@@ -163,6 +163,29 @@ def test_noncanonical_element_inside_a_lane_group(name):
     meas_len = b.vdaf.typ.MEAS_LEN
     lin = b.leader_in.copy()
     bad = {1: meas_len - 1, 3: meas_len // 2, 5: 1}
+    for r, e in bad.items():
+        lin[r, e * es:(e + 1) * es] = 0xFF
+    ls = v.new_state(0, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, lin)
+    for r in range(b.n):
+        if r in bad:
+            assert lst[r] == 8, (r, lst[r])
+        else:
+            assert lst[r] == 0, (r, lst[r])
+            np.testing.assert_array_equal(lp[r], b.leader_prep[r])
+
+
+@pytest.mark.parametrize("name", ["sum8", "sum32", "sum64"])
+def test_noncanonical_gadget_coefficient_rejects_its_report(name):
+    """A non-canonical gadget-polynomial coefficient of the proof share (first, middle, last)
+    rejects only its report in the paired Sum query; every other report's prep share stays
+    bit-exact."""
+    b = batch(name)
+    v = gpu_vdaf(b)
+    es = b.vdaf.fld.ENCODED_SIZE
+    meas_len, proof_len = b.vdaf.typ.MEAS_LEN, b.vdaf.PROOF_LEN
+    lin = b.leader_in.copy()
+    bad = {0: meas_len + 1, 2: meas_len + proof_len // 2, 7: meas_len + proof_len - 1}
     for r, e in bad.items():
         lin[r, e * es:(e + 1) * es] = 0xFF
     ls = v.new_state(0, b.n)
