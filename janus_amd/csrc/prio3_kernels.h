@@ -833,19 +833,25 @@ struct FlpDims {
 //   SMM = sum_k MM[k] | SLM = sum_k LM[k]   (mod p: k_flp_wires_mfma's offset correction)
 // The wire passes finish  wire_2j = L0 s_2j + RP[j] a_j,  wire_2j+1 = L0 s_2j+1 - HL + b_j  from the
 // proof share's wire seeds s themselves (and check them canonical).
+// Every section starts at a multiple of 8 entries (128 B) and a row is a multiple of 8 entries, so
+// k_flp_weights' 8-entry flushes write whole 128-B lines (a flush that straddled two lines left
+// partial lines to be written back twice: 4.23 GB per SumVec launch against 3.52 algorithmic).
+__host__ __device__ inline uint32_t round8(uint32_t x) { return (x + 7u) & ~7u; }
 struct WRow {
-  uint32_t C, c;
-  DEVI explicit WRow(const Cfg& cfg) : C(cfg.calls), c(cfg.chunk) {}
+  uint32_t C8, c8;
+  DEVI explicit WRow(const Cfg& cfg) : C8(round8(cfg.calls)), c8(round8(cfg.chunk)) {}
   DEVI uint32_t mm(uint32_t k0) const { return k0; }  // k0 = k - 1
-  DEVI uint32_t lm(uint32_t k0) const { return C + k0; }
-  DEVI uint32_t rp(uint32_t j) const { return 2 * C + j; }
-  DEVI uint32_t l0() const { return 2 * C + c; }
-  DEVI uint32_t hl() const { return 2 * C + c + 1; }
-  DEVI uint32_t gsum() const { return 2 * C + c + 2; }
-  DEVI uint32_t smm() const { return 2 * C + c + 3; }
-  DEVI uint32_t slm() const { return 2 * C + c + 4; }
+  DEVI uint32_t lm(uint32_t k0) const { return C8 + k0; }
+  DEVI uint32_t rp(uint32_t j) const { return 2 * C8 + j; }
+  DEVI uint32_t l0() const { return 2 * C8 + c8; }
+  DEVI uint32_t hl() const { return 2 * C8 + c8 + 1; }
+  DEVI uint32_t gsum() const { return 2 * C8 + c8 + 2; }
+  DEVI uint32_t smm() const { return 2 * C8 + c8 + 3; }
+  DEVI uint32_t slm() const { return 2 * C8 + c8 + 4; }
 };
-__host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) { return 2 * cfg.calls + cfg.chunk + 5; }
+__host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) {
+  return 2 * round8(cfg.calls) + round8(cfg.chunk) + 8;
+}
 // entries of k_flp_weights' element-major scratch per report: the prefix product at the start of
 // every 8-call block of the batched inversion
 __host__ __device__ inline uint32_t flp_scratch_len(const Cfg& cfg) { return (cfg.calls + 7) / 8; }
@@ -1584,7 +1590,8 @@ __global__ void __launch_bounds__(1024) k_flp_wires(Cfg cfg, uint32_t n, FlpDims
   T* RED = PB + H * c;
   uint32_t* flag = reinterpret_cast<uint32_t*>(RED + nthr);
   if (tid == 0) *flag = 0u;
-  for (uint32_t k = tid; k < 2 * C; k += nthr) MM[k] = FO::load(wm.el(r, k));
+  for (uint32_t k = tid; k < 2 * C; k += nthr)
+    MM[k] = FO::load(wm.el(r, k < C ? W.mm(k) : W.lm(k - C)));
   __syncthreads();
   const uint8_t* xr = meas.at(r);
   bool bad = false;
@@ -1736,7 +1743,7 @@ __global__ void __launch_bounds__(256) k_flp_wires_cols(Cfg cfg, uint32_t n, uin
       x = FO::load(xr + (size_t)idx * ES);
       maybe |= x.w[3] == 0xFFFFFFFFu;
     }
-    const T mm = FO::load(wm.el(rr, k)), lm = FO::load(wm.el(rr, C + k));
+    const T mm = FO::load(wm.el(rr, W.mm(k))), lm = FO::load(wm.el(rr, W.lm(k)));
     wide_mac(wa, mm, x);
     wide_mac(wb, lm, x);
     if (cfg.kind == KIND_HISTOGRAM) {
