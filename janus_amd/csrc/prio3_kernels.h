@@ -927,9 +927,10 @@ DEVI typename FO::T inv_mont(const typename FO::T& x) {
 //     iteration i takes k = i (x_0 = the proof seed), k = calls is the fraction's start;
 //   * p(t) = sum_(i<h) (A_i + t^h A_(i+h)) t^i,  A_i = c_i + t^m c_(i+m): one Horner step per pair;
 //   * the three denominators share one inversion.
-// Per iteration 5 fused + 2 single Montgomery products (mont_fma.h, two interleaved calls)
-// against 5 + 5 for two iterations of the unpaired form (gadget fraction over y_i - 1 with y_i
-// advanced by a product) and 8 + 16 products of the mul3 loop.
+// Per iteration 7 Montgomery products (mont_fma.h, two interleaved calls: the Horner step's four
+// products share ONE reduction, the numerator and wire fractions are fused pairs) against 10 for
+// two iterations of the unpaired form (gadget fraction over y_i - 1 with y_i advanced by a
+// product) and 24 of the mul3 loop.
 // Domains: values marked M are Montgomery form (x R), the rest plain; mont(M, plain) is plain.
 // Operands: iteration i reads c_i, c_(i+m), c_(i+h), c_(i+h+m) (gadget coefficients, proof
 // elements 1 + .) and x_i (measurement element i - 1; x_0 = the proof seed).  A loop trip (i0 + 3
@@ -984,8 +985,8 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
   T X = FO::load(meas.at(min(r0w + lane, n - 1u)) + (size_t)(h - 1) * 16);  // x_calls
   bad |= !FO::is_canonical(X);
   T Nw = X, Dw = FO::sub(tm, ld_tw<FO>(cfg, h));     // plain / M(t - alpha^calls)
-  // Horner's p_(i+1) = P1 + P2 + c_(i+1) is finished inside iteration i's additions
-  T P1 = FO::zero(), P2 = FO::zero(), cprev = FO::zero();
+  // Horner's p_(i+1) = PQ + c_(i+1) is finished inside iteration i's additions
+  T PQ = FO::zero(), cprev = FO::zero();
   stage(h - kSqEl);
   auto step = [&](uint32_t i, auto PAR) {
     constexpr uint32_t par = decltype(PAR)::value;  // = i & 1
@@ -1002,15 +1003,16 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
            !FO::is_canonical(cjm) | !FO::is_canonical(x);
     const uint32_t mi = (m - i) & (m - 1u), m2i = (m - 2u * i) & (m - 1u);
     const T beta = ld_tw<FO>(cfg, mi);                              // M(alpha^-i)
-    T fi, fj, d2, dw, S;
-    // F_i, F_j, M(r^2 - beta^2), M(t - alpha^i), P1 + P2
-    modaddsub_AASSA(ci, cim, fi, cj, cjm, fj, r2, ld_tw<FO>(cfg, m2i), d2, tm, ld_tw<FO>(cfg, i),
-                    dw, P1, P2, S);
+    T fi, fj, d2, dw;
+    // F_i, F_j, M(r^2 - beta^2), M(t - alpha^i)
+    modaddsub_AASS(ci, cim, fi, cj, cjm, fj, r2, ld_tw<FO>(cfg, m2i), d2, tm, ld_tw<FO>(cfg, i),
+                   dw);
     T fs, fd, Xn, pt;
-    modaddsub_ASAA(fi, fj, fs, fi, fj, fd, X, x, Xn, S, cprev, pt);
+    modaddsub_ASAA(fi, fj, fs, fi, fj, fd, X, x, Xn, PQ, cprev, pt);
+    // Horner: t p_(i+1) + t^m c_(i+m) + t^h c_(i+h) + t^(m+h) c_(i+h+m), one reduction
     T U, DN;
-    mont_fma3_mul1(tm, pt, tmm, cim, P1, th, cj, t3h, cjm, P2, rm, fs, beta, fd, U, D[par], d2,
-                   DN);
+    mont_q1_fma1_mul1(tm, pt, tmm, cim, th, cj, t3h, cjm, PQ, rm, fs, beta, fd, U, D[par], d2,
+                      DN);
     T NN, NW, DW;
     mont_fma2_mul1(N[par], d2, U, D[par], NN, Nw, dw, x, Dw, NW, Dw, dw, DW);
     N[par] = NN;
@@ -1027,11 +1029,7 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
     if (i == 1) break;
   }
   T pt;
-  {
-    T S;
-    modaddsub_A(P1, P2, S);
-    modaddsub_A(S, cprev, pt);
-  }
+  modaddsub_A(PQ, cprev, pt);
   // one inversion for Dw, D0, D1
   T t1, t2, t3;
   mul3<FO>(D[0], D[1], Dw, D[1], Dw, D[0], t1, t2, t3);  // M(D0 D1), M(Dw D1), M(Dw D0)

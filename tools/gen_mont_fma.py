@@ -31,13 +31,25 @@ R = 1 << 128
 # ---------------------------------------------------------------------------------------------
 # programs of one operation (register names local to the operation, prefix added later)
 # ---------------------------------------------------------------------------------------------
+# operand pairs of a product sum: M = a b, F = a b + c d, Q = a b + c d + e f + i j
+PAIRS = [("a", "b"), ("c", "d"), ("e", "f"), ("i", "j")]
+KIND_PAIRS = {"M": 1, "F": 2, "Q": 4}
+
+
+def npairs(fused):
+    """number of operand pairs of an operation given as bool (fused) or int"""
+    if isinstance(fused, bool):
+        return 2 if fused else 1
+    return fused
+
+
 def product(fused, rename=False):
     """Column sums of a b (+ c d): L0..L6 (64-bit), carries h0..h6 (32-bit; h_c sits at
     2^(32 c + 64)).  Each mad's carry is read by the addc right after it (the interleave or the
     emitter's s_nop gives the wait states)."""
     ins = []
     first, hset = set(), set()
-    pairs = [("a", "b")] + ([("c", "d")] if fused else [])
+    pairs = PAIRS[:npairs(fused)]
     for (x, y) in pairs:
         for c in range(7):
             for i in range(4):
@@ -105,16 +117,43 @@ def reduce_program(fused):
             A(("subb", Y[i], "k2", Y[i], 0, "k2"))
         return Y
 
-    U = redc(T, 7)  # (T + m p) / 2^64 < 2^194: 7 words
-    V = redc(U, 5)  # < 3 p < 2^130: 5 words
+    U = redc(T, 7)  # (T + m p) / 2^64 < 2^195: 7 words
+    V = redc(U, 5)  # < (np + 1) p: 5 words
+    if npairs(fused) == 4:
+        # V < 5p: fold the top word with 2^128 = c (mod p), c = 28 2^64 - 1, then the modular
+        # add's tail (exclusive flags: a wrap past 2^128 | W >= p) -- V = [l4, l5, l6, g6, h6]
+        A(("lsl", "l0", 5, "h6"))
+        A(("lsl", "l1", 2, "h6"))
+        A(("vsub", "l0", "l0", "l1"))          # t = 28 V4
+        A(("sub_co", "r0", "k", "l4", "h6"))   # W = V_lo - V4 ...
+        A(("subb", "r1", "k", "l5", 0, "k"))
+        A(("subb", "r2", "k", "l6", 0, "k"))
+        A(("subb", "r3", "k", "g6", 0, "k"))
+        A(("subb", "l1", "k", 0, 0, "k"))      # -borrow
+        A(("add_co", "r2", "k2", "r2", "l0"))  # ... + t 2^64
+        A(("addc", "r3", "k2", "r3", 0, "k2"))
+        A(("addc", "l1", "k2", "l1", 0, "k2"))  # e = carry - borrow: W = W_lo + e 2^128
+        A(("add_co", "l2", "k", "r0", -1))     # carry of W_lo + c: W_lo >= p
+        A(("addc", "l2", "k", "r1", -1, "k"))
+        A(("addc", "l2", "k", "r2", 27, "k"))
+        A(("addc", "l2", "k", "r3", 0, "k"))
+        A(("addc", "l1", "k", "l1", 0, "k"))   # sel = e + (W_lo >= p)
+        A(("vsub", "l3", 0, "l1"))
+        A(("and", "l2", 27, "l3"))
+        A(("add_co", "r0", "k", "r0", "l3"))   # r = W_lo + (c & -sel) mod 2^128
+        A(("addc", "r1", "k", "r1", "l3", "k"))
+        A(("addc", "r2", "k", "r2", "l2", "k"))
+        A(("addc", "r3", "k", "r3", 0, "k"))
+        return ins
     # up to two conditional subtractions of p (one suffices for a single product: V < 2p)
-    for rnd in range(2 if fused else 1):
+    nsub = 1 if npairs(fused) == 1 else 2
+    for rnd in range(nsub):
         A(("sub_co", "m0", "k", V[0], 1))
         A(("subb", "a0", "k", V[1], 0, "k"))
         A(("subb", "a1", "k", V[2], "P2", "k"))
         A(("subb", "a2", "k", V[3], -1, "k"))
         A(("subb", "b0", "k", V[4], 0, "k"))  # k = borrow: V < p
-        dst = ["r0", "r1", "r2", "r3", None] if rnd == (1 if fused else 0) else V
+        dst = ["r0", "r1", "r2", "r3", None] if rnd == nsub - 1 else V
         A(("cnd", dst[0], "m0", V[0], "k"))
         A(("cnd", dst[1], "a0", V[1], "k"))
         A(("cnd", dst[2], "a1", V[2], "k"))
@@ -178,11 +217,13 @@ def aliased(prog):
     return [tuple(ALIAS.get(x, x) if isinstance(x, str) else x for x in ins) for ins in prog]
 
 
-def run_op(fused, a, b, c=0, d=0):
+def run_op(fused, *vals):
+    """vals: 2 np operands (a, b[, c, d[, e, f, i, j]])"""
     st = {}
-    for i in range(4):
-        st[f"a{i}"], st[f"b{i}"] = (a >> (32 * i)) & M32, (b >> (32 * i)) & M32
-        st[f"c{i}"], st[f"d{i}"] = (c >> (32 * i)) & M32, (d >> (32 * i)) & M32
+    names = [x for pr in PAIRS[:npairs(fused)] for x in pr]
+    for nm, v in zip(names, vals):
+        for i in range(4):
+            st[f"{nm}{i}"] = (v >> (32 * i)) & M32
     for c in range(7):
         st[f"h{c}"] = 0xDEADBEEF  # garbage: only product_inits are zeroed
     for h in product_inits(fused):
@@ -205,6 +246,11 @@ def check(trials=20000):
         assert run_op(True, a, b, c, d) == (a * b + c * d) * rinv % P, (a, b, c, d)
     for a, b in [(P - 1, P - 1), (P - 2, P - 1)]:  # the largest sums
         assert run_op(True, a, b, a, b) == 2 * a * b * rinv % P
+        assert run_op(4, a, b, a, b, a, b, a, b) == 4 * a * b * rinv % P
+    for t in range(trials):
+        v = [pick(t + k, 3 + k) for k in range(8)]
+        exp = (v[0] * v[1] + v[2] * v[3] + v[4] * v[5] + v[6] * v[7]) * rinv % P
+        assert run_op(4, *v) == exp, v
     return trials
 
 
@@ -371,16 +417,18 @@ def verify_function(ops, progs, sched, rsched, trials=40):
     for t in range(trials):
         init, want, mid = {}, {}, {}
         for s, q, fused, tag in ops:
-            vals = [rng.choice(edge) if (t + k) % 5 == 0 else rng.randrange(P) for k in range(4)]
+            names = [x for pr in PAIRS[:npairs(fused)] for x in pr]
+            vals = [rng.choice(edge) if (t + k) % 5 == 0 else rng.randrange(P)
+                    for k in range(len(names))]
             for i in range(4):
-                for nm, v in zip("abcd", vals):
+                for nm, v in zip(names, vals):
                     init[(tag, f"{nm}{i}")] = (v >> (32 * i)) & M32
             for c in range(7):
                 init[(tag, f"h{c}")] = 0xDEADBEEF
             for h in product_inits(fused):
                 init[(tag, h)] = 0
-            a, b, c_, d = vals
-            want[tag] = (a * b + (c_ * d if fused else 0)) * rinv % P
+            want[tag] = sum(vals[2 * k] * vals[2 * k + 1] for k in range(len(names) // 2)) \
+                * rinv % P
         st = {f"{sid}.{r}": v for (sid, r), v in init.items()}
         check_schedule(sched, init, {})
         # rerun to read the product state, split L into halves for the reduction
@@ -401,19 +449,19 @@ def verify_function(ops, progs, sched, rsched, trials=40):
 
 
 def gen_function(name, spec, volatile=True):
-    """spec: one string per stream of "F" (fused) / "M" (single) operations, e.g. ["F", "F", "MM"].
-    Signature: for every operation in stream order, (a, b[, c, d]) inputs then its output."""
-    ops = []  # (stream, op index in stream, fused, tag)
+    """spec: one string per stream of "M" (a b), "F" (a b + c d) or "Q" (a b + c d + e f + i j)
+    operations, e.g. ["F", "F", "MM"].  Signature: for every operation in stream order, its
+    operand pairs then its output."""
+    ops = []  # (stream, op index in stream, number of operand pairs, tag)
     for s, st in enumerate(spec):
         for q, kind in enumerate(st):
-            ops.append((s, q, kind == "F", f"{s}{q}"))
+            ops.append((s, q, KIND_PAIRS[kind], f"{s}{q}"))
     out = []
     w = out.append
     params = []
     for s, q, fused, tag in ops:
-        params += [f"const F128& a{tag}", f"const F128& b{tag}"]
-        if fused:
-            params += [f"const F128& c{tag}", f"const F128& d{tag}"]
+        for x, y in PAIRS[:fused]:
+            params += [f"const F128& {x}{tag}", f"const F128& {y}{tag}"]
         params.append(f"F128& r{tag}")
     w(f"DEVI void {name}(" + ", ".join(params) + ") {")
     # ---- products ----
@@ -448,11 +496,9 @@ def gen_function(name, spec, volatile=True):
     nout = len(ops_e)
     for s, q, fused, tag in ops:
         for i in range(4):
-            opnd(f"a{i}_{tag}", '"v"', f"a{tag}.w[{i}]")
-            opnd(f"b{i}_{tag}", '"v"', f"b{tag}.w[{i}]")
-            if fused:
-                opnd(f"c{i}_{tag}", '"v"', f"c{tag}.w[{i}]")
-                opnd(f"d{i}_{tag}", '"v"', f"d{tag}.w[{i}]")
+            for x, y in PAIRS[:fused]:
+                opnd(f"{x}{i}_{tag}", '"v"', f"{x}{tag}.w[{i}]")
+                opnd(f"{y}{i}_{tag}", '"v"', f"{y}{tag}.w[{i}]")
 
     def ref(x, tag):
         if isinstance(x, int):
@@ -532,6 +578,12 @@ def gen_function(name, spec, volatile=True):
         elif op == "cnd":
             lines.append(f"v_cndmask_b32_e64 {rref(ins[1], tag)}, {rref(ins[2], tag)}, "
                          f"{rref(ins[3], tag)}, {rref(ins[4], tag)}")
+        elif op == "vsub":
+            lines.append(f"v_sub_u32_e64 {rref(ins[1], tag)}, {rref(ins[2], tag)}, "
+                         f"{rref(ins[3], tag)}")
+        elif op == "and":
+            lines.append(f"v_and_b32_e64 {rref(ins[1], tag)}, {rref(ins[2], tag)}, "
+                         f"{rref(ins[3], tag)}")
         else:
             raise ValueError(op)
     w("  asm volatile(" if volatile else "  asm(")
@@ -689,7 +741,7 @@ def gen_addsub(name, spec, volatile=True):
 
 # one iteration of the Sum FLP query's additions (prio3_kernels.h sum_query_pair)
 ADDSUB = {
-    "modaddsub_AASSA": "AASSA",  # F_i, F_j, r^2 - beta^2, t - alpha^i, the two Horner halves
+    "modaddsub_AASS": "AASS",    # F_i, F_j, r^2 - beta^2, t - alpha^i
     "modaddsub_ASAA": "ASAA",    # F_i + F_j, F_i - F_j, X + x, Horner + c_(i+1)
     "modaddsub_A": "A",
 }
@@ -697,8 +749,9 @@ ADDSUB = {
 
 FUNCTIONS = {
     # one iteration of the Sum FLP query (prio3_kernels.h sum_query_pair), two calls:
-    #   the two Horner halves + the paired numerator + the gadget-output denominator,
-    "mont_fma3_mul1": ["F", "F", "F", "M"],
+    #   the Horner step (four products, one reduction) + the paired numerator + the gadget-output
+    #   denominator,
+    "mont_q1_fma1_mul1": ["Q", "F", "M"],
     #   then the gadget-output fraction's numerator + the wire fraction (numerator, denominator)
     "mont_fma2_mul1": ["F", "F", "M"],
     # k_flp_weights: the forward pass (prefix product + r^j), the backward pass (L_k, the inverse
@@ -716,7 +769,8 @@ if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(root, "janus_amd", "csrc", "mont_fma.h")
     parts = ["// GENERATED by tools/gen_mont_fma.py -- edit the generator, not this file.",
-             "// Field128 Montgomery products r = a b 2^-128 and fused sums r = (a b + c d) 2^-128",
+             "// Field128 Montgomery products r = a b 2^-128 and fused sums r = (a b + c d [+ e f + i j])",
+             "// 2^-128",
              "// (mod p, inputs < p, outputs canonical), several independent operations issued as",
              "// interleaved streams; s_nop only where the interleave leaves a carry hazard.",
              "#pragma once", '#include "field.h"', ""]
