@@ -761,12 +761,15 @@ FUNCTIONS = {
 }
 
 
-if __name__ == "__main__":
-    n = check()
-    print(f"simulated {n} single + {n} fused products: ok "
-          f"(single {len(product(False))} + {len(reduce_program(False))}, "
-          f"fused {len(product(True))} + {len(reduce_program(True))} instructions)")
+def generate(trials=20000, log=print):
+    """Simulate every program, then return {path: text} of the two generated headers (every
+    generated function is also list-scheduled, re-simulated and hazard-checked on the way)."""
+    n = check(trials)
+    log(f"simulated {n} single + {n} fused products: ok "
+        f"(single {len(product(False))} + {len(reduce_program(False))}, "
+        f"fused {len(product(True))} + {len(reduce_program(True))} instructions)")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
     path = os.path.join(root, "janus_amd", "csrc", "mont_fma.h")
     parts = ["// GENERATED by tools/gen_mont_fma.py -- edit the generator, not this file.",
              "// Field128 Montgomery products r = a b 2^-128 and fused sums r = (a b + c d [+ e f + i j])",
@@ -778,18 +781,17 @@ if __name__ == "__main__":
         code, nops = gen_function(name, spec)
         parts.append(f"// streams: {spec}; {nops} s_nop")
         parts.append(code)
-        print(f"{name}: {spec}, {nops} s_nop")
-    n = check_addsub()
-    print(f"simulated {n} modular additions + subtractions: ok "
-          f"({len(modadd_program())} / {len(modsub_program())} instructions)")
+        log(f"{name}: {spec}, {nops} s_nop")
+    n = check_addsub(trials)
+    log(f"simulated {n} modular additions + subtractions: ok "
+        f"({len(modadd_program())} / {len(modsub_program())} instructions)")
     parts.append("// modular additions (A) / subtractions (S), one stream each")
     for name, spec in ADDSUB.items():
         code, nops = gen_addsub(name, spec)
         parts.append(f"// streams: {spec}; {nops} s_nop")
         parts.append(code)
-        print(f"{name}: {spec}, {nops} s_nop")
-    open(path, "w").write("\n".join(parts))
-    print("wrote", path)
+        log(f"{name}: {spec}, {nops} s_nop")
+    out[path] = "\n".join(parts)
     # Field128Ops::add / sub (field.h): one operation, s_nop where its own chain needs them
     path = os.path.join(root, "janus_amd", "csrc", "modadd.h")
     parts = ["// GENERATED by tools/gen_mont_fma.py -- edit the generator, not this file.",
@@ -800,11 +802,17 @@ if __name__ == "__main__":
         code, nops = gen_addsub(name, spec, volatile=False)
         parts.append(f"// {nops} s_nop")
         parts.append(code)
-        print(f"{name}: {spec}, {nops} s_nop")
+        log(f"{name}: {spec}, {nops} s_nop")
     # Field128Ops::mul: one Montgomery product
     code, nops = gen_function("f128_mont_mul1", ["M"], volatile=False)
     parts.append(f"// one Montgomery product; {nops} s_nop")
     parts.append(code)
-    print(f"f128_mont_mul1: {nops} s_nop")
-    open(path, "w").write("\n".join(parts))
-    print("wrote", path)
+    log(f"f128_mont_mul1: {nops} s_nop")
+    out[path] = "\n".join(parts)
+    return out
+
+
+if __name__ == "__main__":
+    for path, text in generate().items():
+        open(path, "w").write(text)
+        print("wrote", path)
