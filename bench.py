@@ -271,12 +271,16 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: the host CPUs this process may use)")
-    ap.add_argument("--overlap", type=int, default=0,
-                    help="1: leader and helper on separate contexts/streams, prepare_init "
-                         "concurrent; 2: pipelined schedule (each batch's FLP query under the "
-                         "other aggregator's Keccak, async contexts, see DESIGN §5); 3: the same "
-                         "with the latency-bound FLP weights kept out from under the Keccak "
-                         "(only the HBM-bound wire pass overlaps)")
+    ap.add_argument("--overlap", type=int, default=-1,
+                    help="0: leader then helper on one context; 1: leader and helper on separate "
+                         "contexts/streams, prepare_init concurrent (like two aggregator "
+                         "processes sharing the GPU); 2: pipelined schedule (each batch's FLP "
+                         "query under the other aggregator's Keccak, async contexts, see DESIGN "
+                         "§5); 3: the same with the latency-bound FLP weights kept out from under "
+                         "the Keccak (only the HBM-bound wire pass overlaps).  -1 (default): the "
+                         "measured best per config -- 1 for Count, Sum and Histogram (their one-"
+                         "lane-per-report sponge launches end in a partly filled wave round that "
+                         "the other aggregator's launch fills), 0 for SumVec")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -295,6 +299,8 @@ def main():
                          "stream) and one contiguous slice of the batch each (Janus "
                          "max_concurrent_job_workers)")
     args = ap.parse_args()
+    if args.overlap < 0:  # profiles/r04/ab_r4u_*.log
+        args.overlap = 0 if args.config == "sumvec" else 1
 
     # One process per GPU.  `--gpus N` without a launcher: start the N ranks ourselves, as a
     # child torch.distributed.run (never exec: nothing here has touched the GPU yet, and the
