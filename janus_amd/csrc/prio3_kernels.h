@@ -549,7 +549,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
   for (int64_t b = 0; b < nblocks; ++b) {
     if (is_fast(b)) {
       if (!P3G_DIAG_JR_NOWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint64_t* L = reinterpret_cast<const uint64_t*>(win + lane * kJrWin);
+      // the lane index re-read per block (2 VALU): nothing lane-derived stays live across the
+      // permutation, so the window and column-sum addresses need no spill slots
+      uint32_t ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      const uint64_t* L = reinterpret_cast<const uint64_t*>(win + ln * kJrWin);
       if (P3G_DIAG_JR_NOABSORB) {
 #pragma unroll
         for (int w = 0; w < 21; ++w) s[w] ^= (uint64_t)b * 0x9E3779B97F4A7C15ull + w;
@@ -566,7 +570,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
         // Speculative accumulation: column sums of the window's 21 new words over the wave's 64
         // rows (lane = word wc + 21 gq, rows gq, gq+3, ...; lane 63's sums are never used), as a
         // 64-bit sum plus carry count.  All reads of a half are issued before the adds.
-        const uint32_t gq = lane / 21u, wc = lane - 21u * gq;
+        const uint32_t gq = ln / 21u, wc = ln - 21u * gq;
         // rows gq + 3i: one base address, the row steps are immediate offsets of ds_read_b64
         const uint8_t* colp = win + 8u * (1u + wc) + gq * kJrWin;
         uint32_t l32 = 0, h32 = 0, cy = 0;
@@ -586,17 +590,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
 #pragma unroll
           for (int i = 0; i < 11; ++i) acc_u64(l32, h32, cy, xs[i]);
         }
-        const uint32_t s1 = (lane + 21u) & 63u, s2 = (lane + 42u) & 63u;
-        const uint32_t la = __shfl(l32, (int)s1, 64), ha = __shfl(h32, (int)s1, 64);
-        const uint32_t ca = __shfl(cy, (int)s1, 64);
-        const uint32_t lb = __shfl(l32, (int)s2, 64), hb = __shfl(h32, (int)s2, 64);
-        const uint32_t cb = __shfl(cy, (int)s2, 64);
-        if (lane < 21u) {
+        // partial sums of lanes ln + 21 and ln + 42 (byte addresses for ds_bpermute)
+        const int s1 = (int)(((ln + 21u) & 63u) << 2), s2 = (int)(((ln + 42u) & 63u) << 2);
+        const uint32_t la = (uint32_t)__builtin_amdgcn_ds_bpermute(s1, (int)l32);
+        const uint32_t ha = (uint32_t)__builtin_amdgcn_ds_bpermute(s1, (int)h32);
+        const uint32_t ca = (uint32_t)__builtin_amdgcn_ds_bpermute(s1, (int)cy);
+        const uint32_t lb = (uint32_t)__builtin_amdgcn_ds_bpermute(s2, (int)l32);
+        const uint32_t hb = (uint32_t)__builtin_amdgcn_ds_bpermute(s2, (int)h32);
+        const uint32_t cb = (uint32_t)__builtin_amdgcn_ds_bpermute(s2, (int)cy);
+        if (ln < 21u) {
           acc_u64(l32, h32, cy, ((uint64_t)ha << 32) | la);
           acc_u64(l32, h32, cy, ((uint64_t)hb << 32) | lb);
-          const size_t at = (size_t)(r0w >> 6) * (size_t)nd + (size_t)(21 * b - 5 + lane);
-          spec_lo[at] = ((uint64_t)h32 << 32) | l32;
-          spec_cy[at] = (uint8_t)(cy + ca + cb);
+          // buffer stores: the wave's row (scalar base) + a 32-bit per-lane offset
+          const size_t wrow = (size_t)(r0w >> 6) * (size_t)nd;
+          const uint32_t at = (uint32_t)(21 * b - 5) + ln;
+          const __amdgpu_buffer_rsrc_t rlo = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(spec_lo + wrow), (short)0, (uint32_t)(8 * nd), kBufRsrcWord3);
+          const __amdgpu_buffer_rsrc_t rcy = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(spec_cy + wrow), (short)0, (uint32_t)nd, kBufRsrcWord3);
+          typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2{l32, h32}, rlo, 8u * at, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(cy + ca + cb), rcy, at, 0, 0);
         }
       }
     } else if (b == 0) {
