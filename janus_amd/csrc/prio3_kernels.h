@@ -1280,16 +1280,28 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
     dw = FO::mul(dw, d);
   }
 
-  // one inversion for both denominators
-  const T inv = inv_mont<FO>(FO::mul(dw, vd));
-  const T dinv = FO::mul(inv, vd), vinv = FO::mul(inv, dw);
-  const T w0 = FO::mul(cm, FO::mul(nw0, dinv));
-  const T v = FO::add(FO::mul(vn, vinv), extra);
+  T w0, w1 = FO::zero(), v;
+  if (cfg.kind == KIND_COUNT && calls + 1u == m) {
+    // Count: the wire terms run over every m-th root of unity, so dw = t^m - 1 and the wire is
+    // (t^m - 1)/m N/dw = N/m; vn = 0, vd = 1: v = extra.  No inversion (the values of a root
+    // t, rejected below, are those of the general path: inv(0) = 0).
+    const T im = ld_tw<FO>(cfg, m);  // 1/m
+    w0 = root ? FO::zero() : FO::mul(nw0, im);
+    if (arity > 1) w1 = root ? FO::zero() : FO::mul(nw1, im);
+    v = extra;
+  } else {
+    // one inversion for both denominators
+    const T inv = inv_mont<FO>(FO::mul(dw, vd));
+    const T dinv = FO::mul(inv, vd), vinv = FO::mul(inv, dw);
+    w0 = FO::mul(cm, FO::mul(nw0, dinv));
+    if (arity > 1) w1 = FO::mul(cm, FO::mul(nw1, dinv));
+    v = FO::add(FO::mul(vn, vinv), extra);
+  }
 
   uint8_t* outp = out_prep.at(r);
   FO::store(outp, v);
   FO::store(outp + ES, w0);
-  if (arity > 1) FO::store(outp + 2 * ES, FO::mul(cm, FO::mul(nw1, dinv)));
+  if (arity > 1) FO::store(outp + 2 * ES, w1);
   FO::store(outp + (size_t)(1 + arity) * ES, pt);
   if (cfg.jr_len > 0) {
     const uint8_t* pp = part.at(r);
