@@ -215,7 +215,9 @@ int prio3gpu_prepare_init(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n, const
  * randomness, the helper's share expansion; VALU-bound Keccak) and the FLP-query phase (weights +
  * one HBM pass over the measurement shares).  prepare_init == xof then query.  Split so a driver
  * can overlap one batch's HBM-bound query with another batch's Keccak on a second context.  The
- * input buffers must stay valid until the query phase. */
+ * input buffers must stay valid until the query phase.  Count has no HBM-bound half: its XOF phase
+ * runs the whole query (one kernel derives t and evaluates the FLP), and its query phase only
+ * copies the prep shares out. */
 int prio3gpu_prepare_init_xof(prio3gpu_ctx* ctx, prio3gpu_state* st, size_t n,
                               const uint8_t* nonces, const uint8_t* public_shares,
                               const uint8_t* input_shares, uint8_t* status);

@@ -258,6 +258,7 @@ struct prio3gpu_state {
   CRows proof_rows{nullptr, 0};  // proof shares (prepare_init_xof -> prepare_init_query)
   bool xof_done = false;         // the XOF phase ran; the query phase is due
   bool weights_done = false;     // ParallelSum: k_flp_weights of the query phase ran already
+  bool query_done = false;       // Count: the XOF phase ran the whole query (fused query rand)
   // speculative accumulation: per-wave column sums of meas-share words, written by k_jr
   DevBuf spec_lo, spec_cy;
   bool spec_ok = false;
@@ -607,6 +608,39 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
   CRows nonces{d_nonces, 16};
   CRows pub{d_pub, g.public_share_len};
   Rows t_rows{st->t.u8(), (size_t)16 * g.qr_len};
+  st->query_done = false;
+  if (g.kind == KIND_COUNT) {
+    // Count: one kernel derives t and runs the whole FLP query (k_flp_query_lane with the nonces):
+    // the short Keccak and the latency-bound query share the launch, and the query phase is empty
+    const size_t in_pitch = input_pitch(st);
+    CRows meas{d_in, in_pitch}, proof{d_in + (size_t)g.meas_len * es, in_pitch};
+    if (st->agg_id != 0) {
+      Rows mo{st->meas.u8(), (size_t)g.meas_len * es};
+      Rows po{st->proof.u8(), (size_t)g.proof_len * es};
+      {
+        PROF(KID_EXPAND);
+        hipLaunchKernelGGL(k_expand<FO>, grid1(n, TPB), dim3(TPB), c->expand_lds, c->stream, g, N,
+                           (uint32_t)st->agg_id, CRows{d_in, in_pitch}, mo, po, d_status);
+      }
+      meas = CRows{mo.base, mo.stride};
+      proof = CRows{po.base, po.stride};
+    }
+    {
+      PROF(KID_FLP_QUERY_LANE);
+      hipLaunchKernelGGL(k_flp_query_lane<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, meas,
+                         proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), 16},
+                         CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
+                         d_nonces, vk_lo, vk_hi);
+    }
+    HIPCHK(hipGetLastError());
+    st->meas_rows = meas;
+    st->proof_rows = proof;
+    st->n = n;
+    st->xof_done = true;
+    st->weights_done = false;
+    st->query_done = true;
+    return 0;
+  }
   {
     PROF(KID_QUERY);
     hipLaunchKernelGGL(k_query_rand<FO>, grid1(n, TPB), dim3(TPB), 0, c->stream, g, N, vk_lo, vk_hi,
@@ -815,6 +849,10 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
     return 0;
   }
   st->xof_done = false;
+  if (st->query_done) {  // Count: ran in the XOF phase
+    st->query_done = false;
+    return 0;
+  }
   if constexpr (FO::ES == 16) {
     if (g.kind == KIND_FPVEC) {
       CHK(launch_fpv_query(c, st, n, meas, proof, d_status));
@@ -835,7 +873,8 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
     PROF(KID_FLP_QUERY_LANE);
     hipLaunchKernelGGL(k_flp_query_lane<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, meas,
                        proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
-                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status);
+                       CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
+                       nullptr, 0ull, 0ull);
   }
   HIPCHK(hipGetLastError());
   return 0;

@@ -138,7 +138,9 @@ template <>
 struct SqueezeVec<Field128Ops> {
   // ESTR: bytes from one output element to the next: 16 (a report's row) or 1024 (element-major
   // 64-report tiles, where a wave's lanes store one contiguous 1 KB per element).
-  template <class Next, uint32_t ESTR = 16>
+  // PRE: the state holds the absorbed (unpermuted) message block; every block's permutation,
+  // the first included, runs at the top of the one loop (a single Keccak copy per call site).
+  template <class Next, uint32_t ESTR = 16, bool PRE = false>
   static DEVI void run(uint64_t s[25], uint32_t n, uint8_t* out, bool exact, Next next) {
     using FO = Field128Ops;
     uint32_t cnt = 0;
@@ -148,6 +150,7 @@ struct SqueezeVec<Field128Ops> {
     uint64_t sink = 0;
 #endif
     while (true) {
+      if constexpr (PRE) next(s);
       bool fast = !exact && cnt + 11u <= n;
       if (parity == 0) {
 #pragma unroll
@@ -214,7 +217,7 @@ struct SqueezeVec<Field128Ops> {
       }
       if (cnt >= n) break;
       parity ^= 1u;
-      next(s);
+      if constexpr (!PRE) next(s);
     }
 #if P3G_DIAG_EXPAND_NOSTORE
     st64(out, sink);
@@ -225,11 +228,12 @@ struct SqueezeVec<Field128Ops> {
 // Field64: 21 whole elements per block, always the per-element path.
 template <>
 struct SqueezeVec<Field64Ops> {
-  template <class Next>
+  template <class Next, uint32_t ESTR = 8, bool PRE = false>
   static DEVI void run(uint64_t s[25], uint32_t n, uint8_t* out, bool /*exact*/, Next next) {
     using FO = Field64Ops;
     uint32_t cnt = 0;
     while (true) {
+      if constexpr (PRE) next(s);
 #pragma unroll
       for (int k = 0; k < 21; ++k) {
         if (cnt < n && s[k] < FO::P) {
@@ -238,7 +242,7 @@ struct SqueezeVec<Field64Ops> {
         }
       }
       if (cnt >= n) break;
-      next(s);
+      if constexpr (!PRE) next(s);
     }
   }
 };
@@ -417,6 +421,31 @@ __global__ void __launch_bounds__(256, P3G_EXPAND_WAVES) k_expand(Cfg cfg, uint3
   if (r >= n) return;
   if (status && status[r] != ST_OK) return;
   const uint8_t* hs = helper_shares.at(r);
+#ifndef P3G_EXPAND_ONECOPY
+#define P3G_EXPAND_ONECOPY 1
+#endif
+#if P3G_EXPAND_ONECOPY && !P3G_DIAG_EXPAND_TILED
+  // proof share, then measurement share, through ONE loop body: the absorb permutation runs inside
+  // the squeeze loop (PRE), so the kernel holds one copy of the unrolled permutation, not four
+  uint32_t ph = 0;
+  asm volatile("" : "+s"(ph));  // opaque trip count: the phase loop is not unrolled
+  for (; ph < 2u; ++ph) {
+    const bool pf = ph == 0u;
+    MsgBlock m;
+    m.clear();
+    m.header(cfg.algo_id, pf ? DST_PROOF_SHARE : DST_MEASUREMENT_SHARE, ld64(hs + (pf ? 16 : 0)),
+             ld64(hs + (pf ? 24 : 8)));
+    m.put8(25, agg_id);
+    m.pad(26, cfg.xof);
+    uint64_t s[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s[i] = i < kRateWords ? m.w[i] : 0ull;
+    SqueezeVec<FO>::template run<KeccakNext, FO::ES, true>(
+        s, pf ? cfg.proof_len : cfg.meas_len, pf ? out_proof.at(r) : out_meas.at(r),
+        cfg.exact_squeeze, KeccakNext{cfg.xof});
+  }
+  return;
+#endif
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), agg_id,
                              cfg.proof_len, out_proof.at(r), cfg.xof, cfg.exact_squeeze);
 #if P3G_DIAG_EXPAND_TILED  // diagnostic: element-major 64-report tiles (consumers not adapted)
@@ -1064,11 +1093,40 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
 #ifndef FLPQ_WAVES  // at least 2 waves/SIMD (<= 256 VGPRs) for the Field128 paired Sum query
 #define FLPQ_WAVES __attribute__((amdgpu_waves_per_eu(2)))
 #endif
+// Count's query randomness inline (k_query_rand's XOF, prio prepare_init): the first canonical
+// word of XOF(verify_key, dst5, nonce), one Keccak copy for the absorb and any further squeeze.
+DEVI F64 query_rand_f64(const Cfg& cfg, uint64_t vk_lo, uint64_t vk_hi, const uint8_t* nz) {
+  MsgBlock mb;
+  mb.clear();
+  mb.header(cfg.algo_id, DST_QUERY_RANDOMNESS, vk_lo, vk_hi);
+  mb.put64(25, ld64(nz));
+  mb.put64(33, ld64(nz + 8));
+  mb.pad(41, cfg.xof);
+  uint64_t s[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) s[i] = i < kRateWords ? mb.w[i] : 0ull;
+  uint64_t v = 0ull;
+  bool found = false;
+  do {
+    keccak_x(s, cfg.xof);
+#pragma unroll
+    for (int k = 0; k < kRateWords; ++k)
+      if (!found && s[k] < Field64Ops::P) {
+        v = s[k];
+        found = true;
+      }
+  } while (!found);
+  return Field64Ops::mk(v);
+}
+
+// qr_nonces != nullptr (Count): t is derived here from the nonce (the XOF phase launches this
+// kernel instead of k_query_rand + a query-phase launch); otherwise t is read from tq.
 template <class FO>
 __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint32_t n, CRows meas,
                                                         CRows proof, CRows tq, CRows jr,
                                                         CRows part, Rows out_prep,
-                                                        uint8_t* status) {
+                                                        uint8_t* status, const uint8_t* qr_nonces,
+                                                        uint64_t vk_lo, uint64_t vk_hi) {
   using T = typename FO::T;
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = r < n && status[r] == ST_OK;
@@ -1088,7 +1146,13 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
   const uint8_t* gp = pr + (size_t)arity * ES;  // gadget poly coefficients
   bool bad = false;
   const T one = FO::one_mont();
-  const T tm = FO::to_mont(FO::load(tq.at(rr)));
+  T traw;
+  if constexpr (FO::ES == 8) {
+    traw = qr_nonces ? query_rand_f64(cfg, vk_lo, vk_hi, qr_nonces + 16u * rr) : FO::load(tq.at(rr));
+  } else {
+    traw = FO::load(tq.at(rr));
+  }
+  const T tm = FO::to_mont(traw);
   T tmm = tm;
   // Sum: t^m, r^m and r^calls (calls < m, right-to-left square-and-multiply) advance together,
   // one triple per bit: t and r squared, r^calls times r^(2^q) (or times one)
