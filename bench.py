@@ -281,6 +281,10 @@ def main():
                          "measured best per config -- 1 for Count, Sum and Histogram (their one-"
                          "lane-per-report sponge launches end in a partly filled wave round that "
                          "the other aggregator's launch fills), 0 for SumVec")
+    ap.add_argument("--async-calls", type=int, default=1,
+                    help="--overlap 0/1: engine calls return once queued (prio3gpu_ctx_set_async; "
+                         "every buffer is device memory), so a step's calls run back to back with "
+                         "no host round trip between them; the two contexts are ordered by marks")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -459,6 +463,12 @@ def main():
         workers.append(wk)
 
     hpool = ThreadPoolExecutor(max_workers=W) if args.overlap else None
+    async_calls = bool(args.async_calls) and args.overlap in (0, 1)
+    if async_calls:
+        for wk in workers:
+            wk.v.set_async(True)
+            if wk.hv is not wk.v:
+                wk.hv.set_async(True)
 
     def run_worker_overlap(wk):
         p, ctx, hctx = wk.p, wk.v._ctx, wk.hv._ctx
@@ -467,8 +477,12 @@ def main():
         check(L.prio3gpu_prepare_init(ctx, wk.ls._h, wk.n, p["nonces"], p["pub"], p["lin"],
                                       p["lprep"], p["lst"]), "leader prepare_init")
         check(fut.result(), "helper prepare_init")
+        if async_calls:  # decide reads the leader's prep shares
+            wk.hv.wait_for(wk.v)
         check(L.prio3gpu_prepare_shares_to_prepare_message(hctx, wk.n, p["lprep"], p["hprep"],
                                                            p["msgs"], p["hst"]), "helper decide")
+        if async_calls:  # the leader's prepare_next reads the prep messages
+            wk.v.wait_for(wk.hv, wk.hv.mark())
 
         def helper_next():
             check(L.prio3gpu_prepare_next(hctx, wk.hs._h, wk.n, p["msgs"], p["hst"], None, None,
@@ -629,8 +643,10 @@ def main():
     total_steps = (max(1, args.warmup) if pipe is not None else args.warmup) + args.steps
     if pipe is not None:
         assert int(pipe["lst"][1].max().item()) == 0, "rejected reports"
-        for v_ in (workers[0].v, workers[0].hv):
-            v_.set_async(False)
+    if pipe is not None or async_calls:
+        for wk in workers:
+            for v_ in (wk.v, wk.hv):
+                v_.set_async(False)
     def total(attr):  # merge the workers' aggregates (mod p) and counts
         acc, cnt = None, 0
         for wk in workers:
@@ -959,7 +975,8 @@ def main():
         "data": f"synthetic: {B} distinct reports/GPU (SURVEY §8(d) recipe; shares made by the GPU "
                 f"client shard), resident in HBM",
         "config": {"workload": label, "xof": "XofTurboShake128" if turbo else "XofShake128",
-                   "engine_options": dict(engine_opts), "schedule": f"overlap {args.overlap}",
+                   "engine_options": dict(engine_opts),
+                   "schedule": f"overlap {args.overlap}" + (", async calls" if async_calls else ""),
                    "reports_per_gpu_per_step": B, "job_workers_per_gpu": W,
                    "parallelism": f"report-sharded x{world}, {W} job stream(s)/GPU, "
                                   + ("RCCL all-gather merge" if args.merge == "rccl" else
