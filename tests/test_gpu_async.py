@@ -8,7 +8,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "sum8"])
+@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "sum8", "count"])
 def test_async_two_context_pipeline_matches_oracle(name):
     import torch
     from janus_amd._lib import check, lib
@@ -258,11 +258,13 @@ def test_rccl_flushes_of_two_async_contexts_on_one_comm():
     comm.close()
 
 
-@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "sumvec_8_1000", "sum8", "fp16_3"])
+@pytest.mark.parametrize("name", ["sumvec_small", "hist256", "sumvec_8_1000", "sum8", "fp16_3",
+                                  "count"])
 def test_three_phase_prepare_init_matches_oracle(name):
     """prepare_init as XOF phase -> weights phase (prio3gpu_prepare_init_weights: ParallelSum
     types' k_flp_weights; a no-op otherwise) -> query phase, for both aggregators: the oracle's
-    prep shares; the weights phase twice is harmless, and the query phase alone still works."""
+    prep shares; the weights phase twice is harmless, and the query phase alone still works.
+    (Count: the XOF phase runs the whole query, the query phase copies the prep shares out.)"""
     from tests.test_gpu_parity import batch, gpu_vdaf
     b = batch(name)  # the transcript tests' cached oracle batch
     v = gpu_vdaf(b)
