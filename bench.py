@@ -282,9 +282,10 @@ def main():
                          "lane-per-report sponge launches end in a partly filled wave round that "
                          "the other aggregator's launch fills), 0 for SumVec")
     ap.add_argument("--async-calls", type=int, default=1,
-                    help="--overlap 0/1: engine calls return once queued (prio3gpu_ctx_set_async; "
-                         "every buffer is device memory), so a step's calls run back to back with "
-                         "no host round trip between them; the two contexts are ordered by marks")
+                    help="--overlap 0/1, one rank: engine calls return once queued "
+                         "(prio3gpu_ctx_set_async; every buffer is device memory), so a step's "
+                         "calls run back to back with no host round trip between them; the two "
+                         "contexts are ordered by marks")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -463,7 +464,8 @@ def main():
         workers.append(wk)
 
     hpool = ThreadPoolExecutor(max_workers=W) if args.overlap else None
-    async_calls = bool(args.async_calls) and args.overlap in (0, 1)
+    # single process only: the multi-rank step keeps the synchronous calls around its RCCL flush
+    async_calls = bool(args.async_calls) and args.overlap in (0, 1) and world == 1
     if async_calls:
         for wk in workers:
             wk.v.set_async(True)
