@@ -287,6 +287,10 @@ def main():
                          "calls run back to back with no host round trip between them; the two "
                          "contexts are ordered by marks")
     ap.add_argument("--helper-only", type=int, default=1, help="also time the helper path alone")
+    ap.add_argument("--prof-steps", type=int, default=2,
+                    help="untimed serial kernel pass after the timed steps (synchronous calls, "
+                         "one kernel at a time): the per-kernel durations behind `roofline` and "
+                         "kernels_ms_per_step (0: use the timed steps' HIP-event spans)")
     ap.add_argument("--hpke", type=int, default=1, help="time the CPU HPKE-open stage (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--xof", default="shake128", choices=["shake128", "turboshake128"],
@@ -583,6 +587,10 @@ def main():
             comm.allreduce(Bv, wk.hpart, wk.hagg)
 
     def step():
+        # the previous step's engine work (async calls on non-blocking HIP streams) reads and
+        # writes these status arrays: drain the device before torch's stream resets them, and
+        # again after, so the engine streams see the reset
+        torch.cuda.synchronize()
         d_lst.zero_()
         d_hst.zero_()
         torch.cuda.synchronize()
@@ -624,31 +632,88 @@ def main():
             step()
     barrier()
     elapsed = time.perf_counter() - t0
-    kt = {}
-    for cx in ctxs:
-        ms = (ctypes.c_double * 64)()
-        nl = (ctypes.c_uint64 * 64)()
-        nk = L.prio3gpu_prof_read(cx, ms, nl, 64)
-        for i in range(nk):
-            if nl[i]:
-                name = L.prio3gpu_prof_kernel_name(i).decode()
-                a, b = kt.get(name, (0.0, 0))
-                kt[name] = (a + ms[i], b + nl[i])
-        check(L.prio3gpu_prof_enable(cx, 0), "prof")
+
+    def read_prof(enable_after):
+        kt_ = {}
+        for cx in ctxs:
+            ms = (ctypes.c_double * 64)()
+            nl = (ctypes.c_uint64 * 64)()
+            nk = L.prio3gpu_prof_read(cx, ms, nl, 64)
+            for i in range(nk):
+                if nl[i]:
+                    name = L.prio3gpu_prof_kernel_name(i).decode()
+                    a, b = kt_.get(name, (0.0, 0))
+                    kt_[name] = (a + ms[i], b + nl[i])
+            check(L.prio3gpu_prof_enable(cx, 1 if enable_after else 0), "prof")
+        return kt_
+
+    # HIP-event spans of the timed schedule: with two contexts co-running (--overlap >= 1) a
+    # kernel's span also covers the time it waited behind, or shared the CUs with, the other
+    # context's kernel, so these are spans, not kernel durations
+    kt_timed = read_prof(args.prof_steps > 0)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    # ---- parity gate: statuses, counts, aggregate == plaintext sum (and == CPU restatement) ------
     assert int(d_lst.max().item()) == 0 and int(d_hst.max().item()) == 0, "rejected reports"
-    total_steps = (max(1, args.warmup) if pipe is not None else args.warmup) + args.steps
     if pipe is not None:
         assert int(pipe["lst"][1].max().item()) == 0, "rejected reports"
     if pipe is not None or async_calls:
         for wk in workers:
             for v_ in (wk.v, wk.hv):
                 v_.set_async(False)
+
+    # ---- serial kernel pass (untimed): the same calls, each synchronous, one after the other
+    # from one thread, so no two kernels share the GPU and each HIP-event span is the kernel's
+    # own duration -- the durations rocprofv3 reports for the same kernels (its PMC passes
+    # serialise dispatches).  The roofline and kernels_ms_per_step come from this pass.
+    def serial_step():
+        torch.cuda.synchronize()
+        d_lst.zero_()
+        d_hst.zero_()
+        torch.cuda.synchronize()
+        for wk in workers:
+            p, ctx, hctx = wk.p, wk.v._ctx, wk.hv._ctx
+            if wk.hv is wk.v:
+                run_worker(wk)
+                continue
+            check(L.prio3gpu_prepare_init(ctx, wk.ls._h, wk.n, p["nonces"], p["pub"], p["lin"],
+                                          p["lprep"], p["lst"]), "leader prepare_init")
+            check(L.prio3gpu_prepare_init(hctx, wk.hs._h, wk.n, p["nonces"], p["pub"], p["hin"],
+                                          p["hprep"], p["hst"]), "helper prepare_init")
+            check(L.prio3gpu_prepare_shares_to_prepare_message(hctx, wk.n, p["lprep"], p["hprep"],
+                                                               p["msgs"], p["hst"]), "decide")
+            check(L.prio3gpu_prepare_next(hctx, wk.hs._h, wk.n, p["msgs"], p["hst"], None, None,
+                                          wk.hpart._h), "helper prepare_next")
+            check(L.prio3gpu_agg_update_reports(wk.hpart._h, wk.n, p["nonces"], p["times"],
+                                                p["hst"], None), "helper report checksums")
+            check(L.prio3gpu_prepare_next(ctx, wk.ls._h, wk.n, p["msgs"], p["lst"], None, None,
+                                          wk.lpart._h), "leader prepare_next")
+            check(L.prio3gpu_agg_update_reports(wk.lpart._h, wk.n, p["nonces"], p["times"],
+                                                p["lst"], None), "leader report checksums")
+        torch.cuda.synchronize()
+        if comm is not None:
+            for wk in workers:
+                comm.allreduce(wk.v, wk.lpart, wk.lagg)
+                comm.allreduce(wk.hv, wk.hpart, wk.hagg)
+
+    serial_el = None
+    if args.prof_steps > 0:
+        barrier()
+        ts0 = time.perf_counter()
+        for _ in range(args.prof_steps):
+            serial_step()
+        barrier()
+        serial_el = time.perf_counter() - ts0
+        kt = read_prof(False)
+        assert int(d_lst.max().item()) == 0 and int(d_hst.max().item()) == 0, "rejected reports"
+    else:
+        kt = kt_timed
+    kt_steps = args.prof_steps if args.prof_steps > 0 else args.steps
+
+    # ---- parity gate: statuses, counts, aggregate == plaintext sum (and == CPU restatement) ------
+    total_steps = ((max(1, args.warmup) if pipe is not None else args.warmup) + args.steps
+                   + max(0, args.prof_steps))
     def total(attr):  # merge the workers' aggregates (mod p) and counts
         acc, cnt = None, 0
         for wk in workers:
@@ -839,10 +904,19 @@ def main():
         roof = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_TOPS, 1),
                 "unit": "Tops/s", "frac": None, "traffic": None, "kernel": dname,
                 "avg_launch_ms": round(avg_launch_s * 1e3, 3)}
+    roof["avg_launch_ms_source"] = ("serial kernel pass" if args.prof_steps > 0
+                                    else "timed steps")
+    if dname in kt_timed and kt_timed[dname][1]:
+        roof["avg_launch_ms_timed_span"] = round(kt_timed[dname][0] / kt_timed[dname][1], 3)
     pm = pmc.get("kernels", {}).get(dname)
     if pm:  # PMC passes of the same command (tools/profile_round.sh), per launch
         roof["traffic"] = pm.get("hbm_bytes_per_launch")
         roof["pmc_source"] = pmc["source"]
+        if roof.get("achieved") and pm.get("avg_ms"):
+            # the same op model over rocprofv3's average duration of this kernel
+            roof["pmc_avg_ms"] = round(pm["avg_ms"], 3)
+            roof["frac_from_pmc_avg_ms"] = round(
+                roof["frac"] * roof["avg_launch_ms"] / pm["avg_ms"], 4)
         if pm.get("SQ_INSTS_VALU"):
             # wave-instructions issued / (launch time x the chip's VALU issue rate)
             roof["valu_issue_frac"] = round(pm["SQ_INSTS_VALU"] / (pm["avg_ms"] / 1e3)
@@ -987,7 +1061,20 @@ def main():
         "cpu_baseline": cpu,
         "hpke_open": hpke_rep,
         "helper_only": helper_only,
-        "kernels_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
+        # each kernel's own duration per step, from the serial kernel pass (one kernel on the GPU
+        # at a time): sums to the serial pass's kernel time, <= its ms_per_step
+        "kernels_ms_per_step": {k: round(v[0] / kt_steps, 3) for k, v in kt.items()},
+        "kernels_source": (f"serial kernel pass, {args.prof_steps} untimed steps after the timed "
+                           f"region (synchronous calls, one kernel on the GPU at a time)"
+                           if args.prof_steps > 0 else "HIP-event spans of the timed steps"),
+        "serial_pass": ({"steps": args.prof_steps,
+                         "ms_per_step": round(serial_el / args.prof_steps * 1e3, 3),
+                         "kernel_ms_per_step": round(sum(v[0] for v in kt.values()) / kt_steps, 3)}
+                        if serial_el else None),
+        # HIP-event spans in the timed (possibly co-running) schedule: a span includes time spent
+        # queued behind or sharing the CUs with the other context's kernels
+        "kernels_timed_span_ms_per_step": {k: round(v[0] / args.steps, 3)
+                                           for k, v in kt_timed.items()},
         "parity": parity,
         "gen_seconds": round(gen_s, 1),
         # the engine build that ran: SHA-256 of its sources + flags (janus_amd/_lib.py)

@@ -11,7 +11,9 @@ mkdir -p "$O" "$R/profiles"
 cd /tmp && export TMPDIR=/tmp
 ARGS="--steps 3 --warmup 1 --cpu-baseline 0 --hpke 0 --helper-only 0 --config $CFG"
 ONE="--steps 1 --warmup 0 --cpu-baseline 0 --hpke 0 --helper-only 0 --config $CFG"
-timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- python3 "$R/bench.py" $ARGS > "$O/trace.log" 2>&1
+# the trace pass runs every kernel alone (--overlap 0: one context, one stream), so its durations
+# are the kernels' own, like the PMC passes (which serialise dispatches) and bench.py's serial pass
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- python3 "$R/bench.py" $ARGS --overlap 0 > "$O/trace.log" 2>&1
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch" -o run -- python3 "$R/bench.py" $ONE > "$O/fetch.log" 2>&1
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write" -o run -- python3 "$R/bench.py" $ONE > "$O/write.log" 2>&1
 timeout -k 10 500 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$O/sq" -o run -- python3 "$R/bench.py" $ONE > "$O/sq.log" 2>&1
