@@ -24,14 +24,24 @@
 //!     (:530-727) becomes one `prio3gpu_prepare_next` + accumulate on it.
 //! * Per-report errors keep Janus's mapping (error.rs:240-300): status 5 -> VdafPrepError,
 //!   8 -> InvalidMessage, 3/4 -> the HPKE errors; a batch call never fails a job for one report.
+//!
+//! The Janus call sites themselves (construction in `TaskAggregator`, the helper's loop, the
+//! leader's job driver, the `gpu:` config sections) are `rust/patches/janus-0.6-mi355x.patch`; the
+//! adapters they use (`GpuConfig`, `HelperBatch`, `LeaderBatch`, `LeaderFinishBatch`, `SlotMap`,
+//! `GpuTaskCache`, `status_of` / `prepare_error`) are at the end of this file.
 pub mod ffi;
 
+use std::collections::HashMap;
 use std::ffi::{c_int, CStr};
+use std::hash::Hash;
 use std::ptr;
 use std::sync::atomic::{AtomicUsize, Ordering};
 use std::sync::{Arc, Mutex, MutexGuard};
 
 use janus_core::task::VdafInstance;
+use janus_messages::PrepareError;
+use prio::topology::ping_pong::PingPongMessage;
+use serde::{Deserialize, Serialize};
 
 /// An engine error (an API failure, not a per-report status).
 #[derive(Debug, Clone)]
@@ -39,6 +49,14 @@ pub struct GpuError {
     pub code: i32,
     pub message: String,
 }
+
+impl std::fmt::Display for GpuError {
+    fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
+        write!(f, "mi355x engine error {}: {}", self.code, self.message)
+    }
+}
+
+impl std::error::Error for GpuError {}
 
 fn check(rc: i32) -> Result<(), GpuError> {
     if rc == 0 {
@@ -132,6 +150,7 @@ pub fn engine_params(vdaf: &VdafInstance) -> Option<EngineParams> {
 pub struct GpuPrio3 {
     ctx: *mut ffi::prio3gpu_ctx,
     pub sizes: ffi::prio3gpu_sizes,
+    kind: c_int,
 }
 
 // A context is moved between tokio blocking threads but never used by two at once (GpuTask
@@ -150,7 +169,38 @@ impl GpuPrio3 {
             unsafe { ffi::prio3gpu_ctx_destroy(ctx) };
             return Err(e);
         }
-        Ok(Self { ctx, sizes })
+        Ok(Self { ctx, sizes, kind: params.kind })
+    }
+
+    /// `Collector::unshard` (collector/src/lib.rs:539-543): the sum of the aggregators' aggregate
+    /// shares mod p, decoded as the instance's aggregate result -- integers for Count, Sum, SumVec
+    /// and Histogram, `d * 2^(1-bits) - num_measurements` per entry for the fixed-point vectors.
+    pub fn unshard(&self, aggregate_shares: &[&[u8]], num_measurements: u64)
+                   -> Result<AggregateResult, GpuError> {
+        let len = self.sizes.aggregate_share as usize;
+        if aggregate_shares.is_empty() || aggregate_shares.iter().any(|a| a.len() != len) {
+            return Err(arg_error(format!("unshard: {} shares of {len} bytes expected",
+                                         aggregate_shares.len())));
+        }
+        let joined = aggregate_shares.concat();
+        let out_len = self.sizes.output_len as usize;
+        if self.kind == ffi::PRIO3GPU_FPVEC {
+            let mut out = vec![0f64; out_len];
+            check(unsafe {
+                ffi::prio3gpu_unshard(self.ctx, joined.as_ptr(), aggregate_shares.len(),
+                                      num_measurements, ptr::null_mut(), out.as_mut_ptr())
+            })?;
+            Ok(AggregateResult::FixedPoint(out))
+        } else {
+            let mut out = vec![0u8; out_len * 16];
+            check(unsafe {
+                ffi::prio3gpu_unshard(self.ctx, joined.as_ptr(), aggregate_shares.len(),
+                                      num_measurements, out.as_mut_ptr(), ptr::null_mut())
+            })?;
+            Ok(AggregateResult::Integers(
+                out.chunks_exact(16).map(|c| u128::from_le_bytes(c.try_into().unwrap())).collect(),
+            ))
+        }
     }
 
     pub fn new_state(&self, agg_id: i32, capacity: usize) -> Result<PrepareState, GpuError> {
@@ -411,22 +461,45 @@ impl GpuTask {
 
     /// The per-report loop of aggregator.rs:1613-1848 for a whole job.  Returns the prep messages
     /// (status 0 -> PrepareStepResult::Continue{Finish{prep_msg}}, else Reject(status)) and the
-    /// per-slot aggregations the datastore transaction (:1889-2044) writes.
+    /// per-slot aggregations the datastore transaction (:1889-2044) writes.  The leader picks the
+    /// job size, so a job larger than the pooled state runs as consecutive engine calls into the
+    /// same aggregate.
     pub fn helper_aggregate_init(&self, job: &HelperJob, status: &mut [u8])
                                  -> Result<(Vec<u8>, Vec<SlotAggregation>), GpuError> {
-        self.check_job(status.len())?;
+        let n = status.len();
+        if n == 0 {
+            return Err(arg_error("empty helper job".into()));
+        }
         let (_, mut guard) = self.acquire();
         let Worker { engine, helper_state, agg, .. } = &mut *guard;
         if helper_state.is_none() {
             *helper_state = Some(engine.new_state(1, self.max_job_size)?);
         }
         let agg = pooled_aggregate(engine, agg, job.slot_count)?;
-        let msgs = engine.helper_init(helper_state.as_mut().unwrap(), job.nonces,
-                                      job.public_shares, job.helper_input_shares,
-                                      job.leader_prep_shares, job.report_times, job.batch_slots,
-                                      status, agg)?;
-        let slots = agg.take(job.slot_count)?;
-        Ok((msgs, slots))
+        let s = self.sizes;
+        let (ps, hs, lp) = (s.public_share as usize, s.helper_input_share as usize,
+                            s.prep_share as usize);
+        let mut run = || -> Result<(Vec<u8>, Vec<SlotAggregation>), GpuError> {
+            let mut msgs = Vec::with_capacity(n * s.prep_msg as usize);
+            let mut lo = 0;
+            while lo < n {
+                let hi = (lo + self.max_job_size).min(n);
+                msgs.extend(engine.helper_init(
+                    helper_state.as_mut().unwrap(), &job.nonces[16 * lo..16 * hi],
+                    &job.public_shares[ps * lo..ps * hi],
+                    &job.helper_input_shares[hs * lo..hs * hi],
+                    &job.leader_prep_shares[lp * lo..lp * hi], &job.report_times[lo..hi],
+                    &job.batch_slots[lo..hi], &mut status[lo..hi], agg)?);
+                lo = hi;
+            }
+            Ok((msgs, agg.take(job.slot_count)?))
+        };
+        let res = run();
+        if res.is_err() {
+            // a failed call may have accumulated part of the job: the pooled aggregate starts clean
+            let _ = agg.reset();
+        }
+        res
     }
 
     /// `step_aggregation_job_aggregate_init` (aggregation_job_driver.rs:290-437) for a whole job:
@@ -660,5 +733,504 @@ impl GpuComm {
 impl Drop for GpuComm {
     fn drop(&mut self) {
         unsafe { ffi::prio3gpu_comm_destroy(self.comm) };
+    }
+}
+
+/// `Collector::unshard`'s aggregate result: `u64` / `u128` / `Vec<u128>` for the integer Prio3
+/// types (Count and Sum have one entry), `Vec<f64>` for the fixed-point vectors.
+#[derive(Debug, Clone, PartialEq)]
+pub enum AggregateResult {
+    Integers(Vec<u128>),
+    FixedPoint(Vec<f64>),
+}
+
+/// The collection-time merge of batch-aggregation shards (aggregate_share.rs:44-66,
+/// `BatchAggregation::merged_with`, models.rs:962-991): `acc` += `src` -- mod-p share sum, count
+/// sum, checksum XOR, interval union.  Host only.
+pub fn merge_slot_aggregations(field_size: u32, acc: &mut SlotAggregation, src: &SlotAggregation)
+                               -> Result<(), GpuError> {
+    if acc.aggregate_share.len() != src.aggregate_share.len() || field_size == 0
+        || acc.aggregate_share.len() % field_size as usize != 0
+    {
+        return Err(arg_error("merge: aggregate shares of different lengths".into()));
+    }
+    let mut src_share = src.aggregate_share.clone();
+    let mut dst = ffi::prio3gpu_batch_aggregation {
+        aggregate_share: acc.aggregate_share.as_mut_ptr(), report_count: acc.report_count,
+        checksum: acc.checksum, interval_start: acc.interval_start,
+        interval_duration: acc.interval_duration,
+    };
+    let from = ffi::prio3gpu_batch_aggregation {
+        aggregate_share: src_share.as_mut_ptr(), report_count: src.report_count,
+        checksum: src.checksum, interval_start: src.interval_start,
+        interval_duration: src.interval_duration,
+    };
+    check(unsafe {
+        ffi::prio3gpu_batch_aggregation_merge(field_size,
+                                              acc.aggregate_share.len() / field_size as usize,
+                                              &mut dst, &from)
+    })?;
+    acc.report_count = dst.report_count;
+    acc.checksum = dst.checksum;
+    acc.interval_start = dst.interval_start;
+    acc.interval_duration = dst.interval_duration;
+    Ok(())
+}
+
+// ------------------------------------------------------------------------------------------------
+// Janus call-site adapters: what rust/patches/janus-0.6-mi355x.patch calls from
+// handle_aggregate_init_generic (aggregator.rs:1613-1848) and the aggregation job driver
+// (aggregation_job_driver.rs:290-437, :530-727).
+// ------------------------------------------------------------------------------------------------
+
+/// The `gpu:` section of the aggregator and aggregation-job-driver configs.  One process per GPU:
+/// `device` is the HIP ordinal this process drives.
+#[derive(Debug, Clone, Copy, PartialEq, Eq, Serialize, Deserialize)]
+pub struct GpuConfig {
+    pub device: i32,
+    /// Engine contexts (HIP streams) per task = aggregation jobs on the GPU at once; the job
+    /// driver's `max_concurrent_job_workers` is the natural value.
+    pub workers: usize,
+    /// Reports per job each pooled state holds.  The leader's `max_aggregation_job_size` must not
+    /// exceed it; the helper splits larger jobs into consecutive calls.
+    pub max_job_size: usize,
+}
+
+impl GpuConfig {
+    /// The task's batched arms (`TaskAggregator::new`, aggregator.rs:797-900), or `None` when the
+    /// VDAF stays on the per-report CPU path (Poplar1, the fake VDAFs) or the verify key is not
+    /// the 16 bytes Prio3 takes.
+    pub fn ops_for(&self, vdaf: &VdafInstance, verify_key: &[u8])
+                   -> Option<Result<GpuVdafOps, GpuError>> {
+        let vk: &[u8; 16] = verify_key.try_into().ok()?;
+        GpuVdafOps::new(vdaf, vk, self.device, self.workers, self.max_job_size)
+    }
+}
+
+/// Engine status of `PrepareError::BatchCollected` (its DAP code, 0, is the engine's "ok").
+const STATUS_BATCH_COLLECTED: u8 = 0xFE;
+
+/// A report's `PrepareError` as the engine's status byte; a non-zero status makes every engine
+/// call skip the report and leave its status as it is.
+pub fn status_of(error: PrepareError) -> u8 {
+    match error {
+        PrepareError::BatchCollected => STATUS_BATCH_COLLECTED,
+        e => e as u8,
+    }
+}
+
+/// The `PrepareError` of a non-zero status.  The engine itself only writes VdafPrepError (5;
+/// every ping-pong failure maps there, error.rs:240-300) and InvalidMessage (8, a non-canonical
+/// element or share length); the other codes come back as the caller set them.
+pub fn prepare_error(status: u8) -> PrepareError {
+    match status {
+        STATUS_BATCH_COLLECTED => PrepareError::BatchCollected,
+        1 => PrepareError::ReportReplayed,
+        2 => PrepareError::ReportDropped,
+        3 => PrepareError::HpkeUnknownConfigId,
+        4 => PrepareError::HpkeDecryptError,
+        6 => PrepareError::BatchSaturated,
+        7 => PrepareError::TaskExpired,
+        8 => PrepareError::InvalidMessage,
+        _ => PrepareError::VdafPrepError,
+    }
+}
+
+/// A job's batch identifiers in first-seen order, numbered as the engine's aggregate slots
+/// (`Accumulator`'s HashMap<BatchIdentifier, BatchData>, accumulator.rs:26-122).
+pub struct SlotMap<K> {
+    keys: Vec<K>,
+    index: HashMap<K, u32>,
+}
+
+impl<K: Clone + Eq + Hash> Default for SlotMap<K> {
+    fn default() -> Self {
+        Self { keys: Vec::new(), index: HashMap::new() }
+    }
+}
+
+impl<K: Clone + Eq + Hash> SlotMap<K> {
+    pub fn new() -> Self {
+        Self::default()
+    }
+
+    pub fn slot_of(&mut self, key: &K) -> u32 {
+        if let Some(&s) = self.index.get(key) {
+            return s;
+        }
+        let s = self.keys.len() as u32;
+        self.keys.push(key.clone());
+        self.index.insert(key.clone(), s);
+        s
+    }
+
+    pub fn len(&self) -> u32 {
+        self.keys.len() as u32
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.keys.is_empty()
+    }
+
+    pub fn into_keys(self) -> Vec<K> {
+        self.keys
+    }
+}
+
+/// Per-report results of one engine call plus the per-slot aggregations, keyed by batch
+/// identifier.
+pub struct JobOutcome<K> {
+    pub status: Vec<u8>,
+    report_ids: Vec<u8>,
+    batch_slots: Vec<u32>,
+    prep_msg_len: usize,
+    prep_msgs: Vec<u8>,
+    pub slots: Vec<(K, SlotAggregation)>,
+}
+
+impl<K> JobOutcome<K> {
+    /// Helper: report `i`'s `PrepareStepResult` payload -- `Continue{Finish{prep_msg}}` (Prio3 is
+    /// one round: the helper finishes in its first step, aggregator.rs:1811-1826) or
+    /// `Reject(error)`.
+    pub fn result(&self, i: usize) -> Result<PingPongMessage, PrepareError> {
+        match self.status[i] {
+            0 => Ok(PingPongMessage::Finish {
+                prep_msg: self.prep_msgs[i * self.prep_msg_len..(i + 1) * self.prep_msg_len]
+                    .to_vec(),
+            }),
+            s => Err(prepare_error(s)),
+        }
+    }
+
+    /// Leader: report `i`'s final state -- `Ok` = Finished and accumulated, else Failed(error).
+    pub fn finished(&self, i: usize) -> Result<(), PrepareError> {
+        match self.status[i] {
+            0 => Ok(()),
+            s => Err(prepare_error(s)),
+        }
+    }
+
+    /// The report IDs accumulated into `slot` (status 0): `BatchData::included_report_ids`, which
+    /// `flush_to_datastore` reports back as unmergeable when the batch was collected meanwhile.
+    pub fn slot_report_ids(&self, slot: usize) -> Vec<[u8; 16]> {
+        (0..self.status.len())
+            .filter(|&i| self.status[i] == 0 && self.batch_slots[i] as usize == slot)
+            .map(|i| self.report_ids[16 * i..16 * i + 16].try_into().unwrap())
+            .collect()
+    }
+}
+
+/// One helper aggregation job gathered for ONE engine call: `handle_aggregate_init_generic`
+/// (aggregator.rs:1613-1848) keeps its per-report HPKE open and decoding, pushes each report
+/// here instead of calling `helper_initialized(..).evaluate(..)` (:1775-1797), and after the loop
+/// runs the job (`prio3gpu_helper_init` + `prio3gpu_agg_update_reports`).
+pub struct HelperBatch<K> {
+    sizes: ffi::prio3gpu_sizes,
+    slots: SlotMap<K>,
+    nonces: Vec<u8>,
+    public_shares: Vec<u8>,
+    helper_input_shares: Vec<u8>,
+    leader_prep_shares: Vec<u8>,
+    report_times: Vec<u64>,
+    batch_slots: Vec<u32>,
+    status: Vec<u8>,
+}
+
+impl<K: Clone + Eq + Hash> HelperBatch<K> {
+    pub fn new(ops: &GpuVdafOps, capacity: usize) -> Self {
+        let s = ops.task().sizes;
+        Self {
+            sizes: s,
+            slots: SlotMap::new(),
+            nonces: Vec::with_capacity(16 * capacity),
+            public_shares: Vec::with_capacity(s.public_share as usize * capacity),
+            helper_input_shares: Vec::with_capacity(s.helper_input_share as usize * capacity),
+            leader_prep_shares: Vec::with_capacity(s.prep_share as usize * capacity),
+            report_times: Vec::with_capacity(capacity),
+            batch_slots: Vec::with_capacity(capacity),
+            status: Vec::with_capacity(capacity),
+        }
+    }
+
+    /// The aggregate slot of a report's batch identifier (`Q::to_batch_identifier`, :1615-1619).
+    pub fn slot_of(&mut self, batch_identifier: &K) -> u32 {
+        self.slots.slot_of(batch_identifier)
+    }
+
+    /// One report, in request order.  `shares`: the encoded public share and the decrypted
+    /// helper input share (`PlaintextInputShare::payload`), or the `PrepareError` the CPU stages
+    /// gave the report (HPKE, decoding: :1633-1770).  `leader_message` must be
+    /// `Initialize{prep_share}`; anything else is a ping-pong mismatch, VdafPrepError.
+    pub fn push(&mut self, report_id: &[u8; 16], time: u64, slot: u32,
+                shares: Result<(&[u8], &[u8]), PrepareError>, leader_message: &PingPongMessage) {
+        let s = &self.sizes;
+        let (pl, hl, ll) = (s.public_share as usize, s.helper_input_share as usize,
+                            s.prep_share as usize);
+        let mut st = 0u8;
+        let (public_share, input_share) = match shares {
+            Ok((p, h)) if p.len() == pl && h.len() == hl => (p, h),
+            Ok(_) => {
+                st = status_of(PrepareError::InvalidMessage);
+                (&[][..], &[][..])
+            }
+            Err(e) => {
+                st = status_of(e);
+                (&[][..], &[][..])
+            }
+        };
+        let prep_share = match leader_message {
+            PingPongMessage::Initialize { prep_share } if prep_share.len() == ll => {
+                Some(prep_share.as_slice())
+            }
+            _ => None,
+        };
+        if st == 0 && prep_share.is_none() {
+            st = status_of(PrepareError::VdafPrepError);
+        }
+        let fill = |v: &mut Vec<u8>, b: &[u8], len: usize| {
+            if st == 0 {
+                v.extend_from_slice(b);
+            } else {
+                v.resize(v.len() + len, 0);
+            }
+        };
+        self.nonces.extend_from_slice(report_id);
+        fill(&mut self.public_shares, public_share, pl);
+        fill(&mut self.helper_input_shares, input_share, hl);
+        fill(&mut self.leader_prep_shares, prep_share.unwrap_or(&[]), ll);
+        self.report_times.push(time);
+        self.batch_slots.push(slot);
+        self.status.push(st);
+    }
+
+    pub fn len(&self) -> usize {
+        self.status.len()
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.status.is_empty()
+    }
+
+    /// The job on the GPU: per-report results and the per-batch-identifier aggregations.
+    pub fn run(mut self, ops: &GpuVdafOps) -> Result<JobOutcome<K>, GpuError> {
+        let prep_msg_len = self.sizes.prep_msg as usize;
+        let (prep_msgs, slots) = if self.status.is_empty() {
+            (Vec::new(), Vec::new())
+        } else {
+            let job = HelperJob {
+                nonces: &self.nonces, public_shares: &self.public_shares,
+                helper_input_shares: &self.helper_input_shares,
+                leader_prep_shares: &self.leader_prep_shares, report_times: &self.report_times,
+                batch_slots: &self.batch_slots, slot_count: self.slots.len(),
+            };
+            ops.helper_aggregate_init(&job, &mut self.status)?
+        };
+        Ok(JobOutcome {
+            status: self.status, report_ids: self.nonces, batch_slots: self.batch_slots,
+            prep_msg_len, prep_msgs, slots: self.slots.into_keys().into_iter().zip(slots).collect(),
+        })
+    }
+}
+
+/// The leader's job between `prepare_init` and the helper's response: the prep shares that go
+/// into the `PrepareInit` messages and the job's device state.
+pub struct LeaderInitOutcome {
+    status: Vec<u8>,
+    report_ids: Vec<u8>,
+    report_times: Vec<u64>,
+    prep_share_len: usize,
+    prep_shares: Vec<u8>,
+    /// `None` for a job with no report left after the per-report checks
+    pending: Option<LeaderPending>,
+}
+
+impl LeaderInitOutcome {
+    /// Report `i`'s `PingPongMessage::Initialize` for the AggregationJobInitializeReq
+    /// (aggregation_job_driver.rs:381-394), or the PrepareError it failed with (:395-400).
+    pub fn message(&self, i: usize) -> Result<PingPongMessage, PrepareError> {
+        match self.status[i] {
+            0 => Ok(PingPongMessage::Initialize {
+                prep_share: self.prep_shares[i * self.prep_share_len..(i + 1) * self.prep_share_len]
+                    .to_vec(),
+            }),
+            s => Err(prepare_error(s)),
+        }
+    }
+}
+
+/// The leader's `step_aggregation_job_aggregate_init` loop (aggregation_job_driver.rs:329-402):
+/// the reports that passed the per-report checks, then ONE `prio3gpu_prepare_init(agg_id 0)`.
+pub struct LeaderBatch {
+    sizes: ffi::prio3gpu_sizes,
+    nonces: Vec<u8>,
+    public_shares: Vec<u8>,
+    leader_input_shares: Vec<u8>,
+    report_times: Vec<u64>,
+}
+
+impl LeaderBatch {
+    pub fn new(ops: &GpuVdafOps, capacity: usize) -> Self {
+        let s = ops.task().sizes;
+        Self {
+            sizes: s,
+            nonces: Vec::with_capacity(16 * capacity),
+            public_shares: Vec::with_capacity(s.public_share as usize * capacity),
+            leader_input_shares: Vec::with_capacity(s.leader_input_share as usize * capacity),
+            report_times: Vec::with_capacity(capacity),
+        }
+    }
+
+    /// One `LeaderStoredReport`: its encoded public share and leader input share
+    /// (`get_encoded()` of the decoded values, aggregator_core/src/datastore.rs:1298-1304).  A
+    /// share of the wrong length fails the report with InvalidMessage.
+    pub fn push(&mut self, report_id: &[u8; 16], time: u64, public_share: &[u8],
+                leader_input_share: &[u8]) {
+        let s = &self.sizes;
+        let ok = public_share.len() == s.public_share as usize
+            && leader_input_share.len() == s.leader_input_share as usize;
+        self.nonces.extend_from_slice(report_id);
+        if ok {
+            self.public_shares.extend_from_slice(public_share);
+            self.leader_input_shares.extend_from_slice(leader_input_share);
+        } else {
+            // an all-zero leader share is never a valid report: the engine rejects it, and
+            // `run` marks it InvalidMessage first
+            let (pl, ll) = (s.public_share as usize, s.leader_input_share as usize);
+            self.public_shares.resize(self.public_shares.len() + pl, 0);
+            self.leader_input_shares.resize(self.leader_input_shares.len() + ll, 0);
+        }
+        self.report_times.push(if ok { time } else { u64::MAX });
+    }
+
+    pub fn len(&self) -> usize {
+        self.report_times.len()
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.report_times.is_empty()
+    }
+
+    pub fn run(self, ops: &GpuVdafOps) -> Result<LeaderInitOutcome, GpuError> {
+        let mut status: Vec<u8> = self
+            .report_times
+            .iter()
+            .map(|&t| if t == u64::MAX { status_of(PrepareError::InvalidMessage) } else { 0 })
+            .collect();
+        let (prep_shares, pending) = if status.is_empty() {
+            (Vec::new(), None)
+        } else {
+            let job = LeaderInitJob {
+                nonces: &self.nonces, public_shares: &self.public_shares,
+                leader_input_shares: &self.leader_input_shares,
+            };
+            let (prep, pending) = ops.leader_aggregate_init(&job, &mut status)?;
+            (prep, Some(pending))
+        };
+        Ok(LeaderInitOutcome {
+            status, report_ids: self.nonces, report_times: self.report_times,
+            prep_share_len: self.sizes.prep_share as usize, prep_shares, pending,
+        })
+    }
+}
+
+/// `process_response_from_helper` (aggregation_job_driver.rs:530-727) for a GPU-initialised
+/// job: the helper's `PrepareResp`s gathered per report, then ONE `prio3gpu_prepare_next` +
+/// accumulate + report bookkeeping.
+pub struct LeaderFinishBatch<K> {
+    init: LeaderInitOutcome,
+    prep_msg_len: usize,
+    prep_msgs: Vec<u8>,
+    batch_slots: Vec<u32>,
+    slots: SlotMap<K>,
+}
+
+impl<K: Clone + Eq + Hash> LeaderFinishBatch<K> {
+    pub fn new(ops: &GpuVdafOps, init: LeaderInitOutcome) -> Self {
+        let n = init.status.len();
+        let pm = ops.task().sizes.prep_msg as usize;
+        Self { init, prep_msg_len: pm, prep_msgs: vec![0u8; n * pm], batch_slots: vec![0; n],
+               slots: SlotMap::new() }
+    }
+
+    /// The helper's answer for report `i` (an index into the init batch): `Ok(message)` for
+    /// `PrepareStepResult::Continue{message}` -- a Prio3 helper answers Finish{prep_msg}; any
+    /// other message is a ping-pong mismatch (VdafPrepError) -- or the error the caller mapped
+    /// (`Reject(err)` -> err; `Finished` while the leader is still continued -> VdafPrepError,
+    /// :632-664).  `batch_identifier`: `Q::to_batch_identifier` of the report's time.
+    pub fn push(&mut self, i: usize, batch_identifier: &K,
+                helper_message: Result<&PingPongMessage, PrepareError>) {
+        self.batch_slots[i] = self.slots.slot_of(batch_identifier);
+        if self.init.status[i] != 0 {
+            return;
+        }
+        let pm = self.prep_msg_len;
+        self.init.status[i] = match helper_message {
+            Ok(PingPongMessage::Finish { prep_msg }) if prep_msg.len() == pm => {
+                self.prep_msgs[i * pm..(i + 1) * pm].copy_from_slice(prep_msg);
+                0
+            }
+            Ok(_) => status_of(PrepareError::VdafPrepError),
+            Err(e) => status_of(e),
+        };
+    }
+
+    /// Reports of the init batch (pushed or not: a report that failed at init, and so was not
+    /// sent, keeps its status).
+    pub fn len(&self) -> usize {
+        self.init.status.len()
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.init.status.is_empty()
+    }
+
+    pub fn run(self, ops: &GpuVdafOps) -> Result<JobOutcome<K>, GpuError> {
+        let Self { init, prep_msg_len, prep_msgs, batch_slots, slots } = self;
+        let LeaderInitOutcome { mut status, report_ids, report_times, pending, .. } = init;
+        let aggs = match pending {
+            None => Vec::new(),
+            Some(pending) => {
+                let job = LeaderFinishJob {
+                    prep_msgs: &prep_msgs, nonces: &report_ids, report_times: &report_times,
+                    batch_slots: &batch_slots, slot_count: slots.len().max(1),
+                };
+                ops.leader_process_response(pending, &job, &mut status)?
+            }
+        };
+        Ok(JobOutcome {
+            status, report_ids, batch_slots, prep_msg_len, prep_msgs,
+            slots: slots.into_keys().into_iter().zip(aggs).collect(),
+        })
+    }
+}
+
+/// The aggregation job driver's engines, one `GpuVdafOps` per (task, verify key), created on
+/// first use (the driver has no `TaskAggregator` cache; aggregation_job_driver.rs:102-119 builds
+/// the VDAF per job).
+pub struct GpuTaskCache {
+    cfg: GpuConfig,
+    tasks: Mutex<HashMap<(Vec<u8>, Vec<u8>), Option<Arc<GpuVdafOps>>>>,
+}
+
+impl GpuTaskCache {
+    pub fn new(cfg: GpuConfig) -> Self {
+        Self { cfg, tasks: Mutex::new(HashMap::new()) }
+    }
+
+    /// `None` for VDAFs that stay on the CPU path.  An engine failure is returned, not cached.
+    pub fn ops_for(&self, task_id: &[u8], vdaf: &VdafInstance, verify_key: &[u8])
+                   -> Result<Option<Arc<GpuVdafOps>>, GpuError> {
+        let key = (task_id.to_vec(), verify_key.to_vec());
+        let mut tasks = self.tasks.lock().unwrap();
+        if let Some(ops) = tasks.get(&key) {
+            return Ok(ops.clone());
+        }
+        let ops = match self.cfg.ops_for(vdaf, verify_key) {
+            None => None,
+            Some(Ok(ops)) => Some(Arc::new(ops)),
+            Some(Err(e)) => return Err(e),
+        };
+        tasks.insert(key, ops.clone());
+        Ok(ops)
     }
 }
