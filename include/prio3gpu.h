@@ -290,7 +290,12 @@ int prio3gpu_batch_aggregation_merge(uint32_t field_size, size_t output_len,
  * 128-bit).  Counts are summed with an RCCL uint64 all-reduce.
  * agg_allreduce: total += sum over ranks of local, then local is reset (the per-GPU partial of one
  * aggregation job is flushed into the running aggregate, like Accumulator::flush_to_datastore,
- * accumulator.rs:133-215).  With total == NULL, local is replaced by the sum over ranks. */
+ * accumulator.rs:133-215).  With total == NULL, local is replaced by the sum over ranks.
+ * agg_allreduce is a collective per call: every rank must issue its flushes on a communicator in
+ * the same order with the same slot count.  Within a process the communicator serialises
+ * concurrent contexts, but across processes nothing orders them -- concurrent job workers that
+ * flush per job need one communicator each (or prio3gpu_agg_epoch_merge below, which keeps the
+ * partials across jobs and merges once per epoch). */
 int prio3gpu_comm_unique_id(uint8_t out_id[128]);
 int prio3gpu_comm_init(const uint8_t id[128], int nranks, int rank, int device,
                        prio3gpu_comm** out);
@@ -298,34 +303,30 @@ int prio3gpu_comm_destroy(prio3gpu_comm* comm);
 int prio3gpu_agg_allreduce(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg* local,
                            prio3gpu_agg* total);
 
+/* Epoch merge: the multi-GPU contract for independent job drivers.  Each GPU keeps its partial
+ * aggregate across ANY number of jobs (its own slots, keyed by the batch identifiers it saw) and
+ * the ranks merge once per epoch -- a collection boundary, as aggregate_share.rs:44-66 merges the
+ * batch-aggregation shards -- instead of in lockstep per job:
+ *   slot_map[s]   for each of local's slots, its index in the epoch's union slot table
+ *                 (union_slots entries: the sorted union of every rank's batch identifiers,
+ *                 agreed over the caller's host channel, the same on every rank); injective,
+ *                 < union_slots, or PRIO3GPU_SLOT_UNUSED for a slot no job of the epoch used
+ *   total         union_slots slots; total[slot_map[s]] += sum over ranks of local[s] (mod p,
+ *                 counts, checksum XOR, interval union, folded in rank order), then local is reset
+ * Ordering contract: a collective over `comm`.  Every rank calls it once per epoch with epochs in
+ * the same order, from ONE thread per communicator, and no other flush (agg_allreduce) is in
+ * flight on that communicator -- give each merger (task x aggregator role) its own communicator
+ * or serialise them.  Synchronous: returns after the merge has completed on this rank. */
+#define PRIO3GPU_SLOT_UNUSED 0xFFFFFFFFu
+int prio3gpu_agg_epoch_merge(prio3gpu_comm* comm, prio3gpu_ctx* ctx, prio3gpu_agg* local,
+                             const uint32_t* slot_map, uint32_t union_slots, prio3gpu_agg* total);
+
 /* Per-kernel timing with HIP events on the context's stream (opt-in; bench.py uses it for the
  * live roofline numbers).  prof_read returns min(kernel ids, max_kernels) and fills, per kernel id,
  * the summed milliseconds and launch count since the last read. */
 int prio3gpu_prof_enable(prio3gpu_ctx* ctx, int on);
 int prio3gpu_prof_read(prio3gpu_ctx* ctx, double* ms, uint64_t* launches, int max_kernels);
 const char* prio3gpu_prof_kernel_name(int kernel_id);
-
-/* TEST ONLY.  The XOF squeeze every kernel runs (prio `into_field_vec`, reached through
- * XofShake128::next_vec: ES-byte LE chunks, reject >= p) over caller-crafted rate blocks instead
- * of Keccak output: blocks[25 i .. 25 i + 25) is the state after the i-th permutation (words
- * 0..20 are the 168-byte rate block).  field_size 8 or 16; exact != 0 forces the per-element path
- * (as PRIO3GPU_EXACT_SQUEEZE=1 does in the real kernels).  Runs on the current HIP device. */
-int prio3gpu_test_squeeze(int field_size, const uint64_t* blocks, size_t nblocks, uint32_t n,
-                          uint8_t* out, int exact);
-/* TEST ONLY.  The FLP-query phase of prepare_init (agg_id 0) over caller-supplied randomness
- * instead of the XOF's: leader_input_shares n x leader_input_share, query_rand n x qr_len x
- * field_size (qr_len = 1, 2 for FixedPoint), joint_rand n x joint_rand_len x field_size, own_parts
- * n x 16 (the prep share's joint-rand part).  Writes the prep shares; a query point that is a root
- * of unity sets status 5 (VdafPrepError), as prio does.  Lets tests reach the branches that
- * SHAKE128 output reaches with negligible probability (t^m == 1, r^m == 1). */
-int prio3gpu_test_flp_query(prio3gpu_ctx* ctx, size_t n, const uint8_t* leader_input_shares,
-                            const uint8_t* query_rand, const uint8_t* joint_rand,
-                            const uint8_t* own_parts, uint8_t* out_prep_shares, uint8_t* status);
-
-/* Device memory helpers (bench / tests that stage inputs in HBM without torch). */
-int prio3gpu_dev_alloc(prio3gpu_ctx* ctx, size_t bytes, void** out);
-int prio3gpu_dev_free(prio3gpu_ctx* ctx, void* p);
-int prio3gpu_memcpy(prio3gpu_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 /* ---- DAP codec edge (host-only; janus_amd/csrc/codec.cpp) ------------------------------------
  * Batched decode/encode of the aggregate-init messages around the engine,

@@ -49,7 +49,8 @@ def source_hash(csrc: Path = CSRC, include: Path = INCLUDE, flags=FLAGS) -> str:
     contents it was built from are unchanged)."""
     import hashlib
     h = hashlib.sha256()
-    files = [csrc / s for s in SOURCES] + sorted(csrc.glob("*.h")) + [include / "prio3gpu.h"]
+    files = ([csrc / s for s in SOURCES] + sorted(csrc.glob("*.h"))
+             + [include / "prio3gpu.h", include / "prio3gpu_test.h"])
     for p in files:
         h.update(p.name.encode() + b"\0" + p.read_bytes() + b"\0")
     h.update(" ".join(flags + LIBS).encode())
@@ -133,6 +134,7 @@ def _declare(lib):
         "prio3gpu_comm_init": (c.c_int, [u8p, c.c_int, c.c_int, c.c_int, c.POINTER(P)]),
         "prio3gpu_comm_destroy": (c.c_int, [P]),
         "prio3gpu_agg_allreduce": (c.c_int, [P, P, P, P]),
+        "prio3gpu_agg_epoch_merge": (c.c_int, [P, P, P, P, c.c_uint32, P]),
         "prio3gpu_prof_enable": (c.c_int, [P, c.c_int]),
         "prio3gpu_prof_read": (c.c_int, [P, P, P, c.c_int]),
         "prio3gpu_prof_kernel_name": (c.c_char_p, [c.c_int]),
@@ -141,6 +143,7 @@ def _declare(lib):
         "prio3gpu_dev_alloc": (c.c_int, [P, c.c_size_t, c.POINTER(P)]),
         "prio3gpu_dev_free": (c.c_int, [P, P]),
         "prio3gpu_memcpy": (c.c_int, [P, P, P, c.c_size_t]),
+        "prio3gpu_test_hpke_set_ifma": (c.c_int, [c.c_int]),
         "prio3gpu_last_error": (c.c_char_p, []),
         "prio3gpu_build_hash": (c.c_char_p, []),
         "prio3gpu_unshard": (c.c_int, [P, u8p, c.c_size_t, c.c_uint64, u8p, P]),
@@ -186,7 +189,7 @@ def _declare(lib):
     return sigs
 
 
-# Every symbol include/prio3gpu.h declares (checked by tests/test_abi.py).
+# Every symbol include/prio3gpu.h declares (the product ABI; checked by tests/test_abi.py).
 EXPORTED = [
     "prio3gpu_ctx_create", "prio3gpu_ctx_create2", "prio3gpu_ctx_destroy", "prio3gpu_ctx_sizes",
     "prio3gpu_ctx_sync", "prio3gpu_ctx_set_async", "prio3gpu_ctx_set_option", "prio3gpu_ctx_wait",
@@ -200,14 +203,20 @@ EXPORTED = [
     "prio3gpu_prepare_init",
     "prio3gpu_prepare_shares_to_prepare_message", "prio3gpu_prepare_next", "prio3gpu_helper_init",
     "prio3gpu_random_size", "prio3gpu_shard", "prio3gpu_comm_unique_id", "prio3gpu_comm_init", "prio3gpu_comm_destroy",
-    "prio3gpu_agg_allreduce", "prio3gpu_prof_enable", "prio3gpu_prof_read",
-    "prio3gpu_prof_kernel_name", "prio3gpu_test_squeeze", "prio3gpu_test_flp_query", "prio3gpu_dev_alloc", "prio3gpu_dev_free", "prio3gpu_memcpy",
+    "prio3gpu_agg_allreduce", "prio3gpu_agg_epoch_merge", "prio3gpu_prof_enable",
+    "prio3gpu_prof_read",
+    "prio3gpu_prof_kernel_name",
     "prio3gpu_last_error", "prio3gpu_build_hash", "prio3gpu_unshard", "prio3gpu_decode_agg_init_req", "prio3gpu_gather_prepare_inits",
     "prio3gpu_apply_faults", "prio3gpu_check_agg_init_req", "prio3gpu_batch_aggregation_merge",
     "prio3gpu_decode_plaintext_input_shares", "prio3gpu_encode_agg_job_resp",
     "prio3gpu_encode_agg_init_req", "prio3gpu_decode_agg_job_resp", "prio3gpu_gather_helper_resps",
     "prio3gpu_hpke_open", "prio3gpu_hpke_seal", "prio3gpu_hpke_public_key",
     "prio3gpu_hpke_open_report_shares", "prio3gpu_x25519_batch",
+]
+# The test / benchmark hooks of include/prio3gpu_test.h (same library, not part of the product ABI).
+TEST_EXPORTED = [
+    "prio3gpu_test_squeeze", "prio3gpu_test_flp_query", "prio3gpu_dev_alloc", "prio3gpu_dev_free",
+    "prio3gpu_memcpy", "prio3gpu_test_hpke_set_ifma",
 ]
 
 

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/prio3gpu.h"
+#include "../../include/prio3gpu_test.h"
 #include "errors.h"
 #include "prio3_kernels.h"
 #include "fpvec_kernels.h"
@@ -674,7 +675,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     bool fused_done = false;
     if constexpr (FO::ES == 16) {
       // Few huge reports: the two helper sponges (expansion, joint-rand part) in lockstep.
-      if (g.kind == KIND_FPVEC && c->fused_helper && g.jr_len > 0) {
+      if (g.kind == KIND_FPVEC && c->fused_helper && !g.exact_squeeze && g.jr_len > 0) {
         CHK(c->fallback.ensure(4));
         uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
         HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
@@ -871,7 +872,8 @@ int launch_prep_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, uint8_t* d_
   }
   {
     PROF(KID_FLP_QUERY_LANE);
-    hipLaunchKernelGGL(k_flp_query_lane<FO>, grid1(n, 256), dim3(256), 0, c->stream, g, N, meas,
+    hipLaunchKernelGGL(k_flp_query_lane<FO>, grid1(n, 256), dim3(256),
+                       flpq_pair(g) ? kFlpqPairLds : 0u, c->stream, g, N, meas,
                        proof, CRows{st->t.u8(), 16}, CRows{st->jr.u8(), (size_t)g.jr_len * es},
                        CRows{st->part.u8(), 16}, Rows{st->prep.u8(), g.prep_share_len}, d_status,
                        nullptr, 0ull, 0ull);
@@ -1622,7 +1624,6 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
     // every XOF squeeze takes the exact per-element rejection path (test switch); the FixedPoint
     // helper then runs its exact two-pass XOF
     c->cfg.exact_squeeze = on ? 1u : 0u;
-    if (on) c->fused_helper = false;
   } else {
     set_err("unknown engine option \"%s\"", name);
     return PRIO3GPU_E_ARG;
@@ -2081,6 +2082,55 @@ int prio3gpu_agg_allreduce(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* loc
     HIPCHK(hipGetLastError());
   }
   return finish_call(c, {});
+}
+
+int prio3gpu_agg_epoch_merge(prio3gpu_comm* cm, prio3gpu_ctx* c, prio3gpu_agg* local,
+                             const uint32_t* slot_map, uint32_t union_slots, prio3gpu_agg* total) {
+  if (!cm || !c || !local || !total || local->ctx != c || total->ctx != c ||
+      total->slots != union_slots || union_slots == 0 || !slot_map) {
+    set_err("epoch merge: bad argument");
+    return PRIO3GPU_E_ARG;
+  }
+  std::vector<uint8_t> seen(union_slots, 0);
+  for (uint32_t s = 0; s < local->slots; ++s) {
+    if (slot_map[s] == PRIO3GPU_SLOT_UNUSED) continue;
+    if (slot_map[s] >= union_slots || seen[slot_map[s]]++) {
+      set_err("epoch merge: slot_map[%u] = %u is out of range or repeated", s, slot_map[s]);
+      return PRIO3GPU_E_ARG;
+    }
+  }
+  HIPCHK(hipSetDevice(c->device));
+  // the partial laid out by the epoch's union slot table, identical on every rank
+  prio3gpu_agg* stage = nullptr;
+  CHK(prio3gpu_agg_create(c, union_slots, &stage));
+  DevBuf dmap;
+  int rc = dmap.ensure((size_t)local->slots * 4);
+  if (rc == 0) rc = hipMemcpyAsync(dmap.p, slot_map, (size_t)local->slots * 4,
+                                   hipMemcpyHostToDevice, c->stream) == hipSuccess
+                        ? 0 : PRIO3GPU_E_HIP;
+  if (rc == 0) {
+    const size_t row_words = (size_t)c->cfg.out_len * c->cfg.es / 8;
+    const uint32_t bx = (uint32_t)std::min<size_t>((row_words + 255) / 256, 64);
+    hipLaunchKernelGGL(k_agg_scatter, dim3(bx, local->slots), dim3(256), 0, c->stream,
+                       reinterpret_cast<uint64_t*>(stage->share.p),
+                       reinterpret_cast<unsigned long long*>(stage->counts.p),
+                       reinterpret_cast<SlotMeta*>(stage->meta.p),
+                       reinterpret_cast<const uint64_t*>(local->share.p),
+                       reinterpret_cast<const unsigned long long*>(local->counts.p),
+                       reinterpret_cast<const SlotMeta*>(local->meta.p),
+                       reinterpret_cast<const uint32_t*>(dmap.p), row_words);
+    rc = hipGetLastError() == hipSuccess ? 0 : PRIO3GPU_E_HIP;
+  }
+  if (rc == 0) rc = prio3gpu_agg_allreduce(cm, c, stage, total);  // total += sum_r stage_r
+  if (rc == 0) rc = prio3gpu_agg_reset(local);  // the epoch's partial is flushed
+  // the staging buffers are freed only after the stream has used them
+  const bool synced = hipStreamSynchronize(c->stream) == hipSuccess;
+  prio3gpu_agg_destroy(stage);
+  if (rc == 0 && !synced) {
+    set_err("epoch merge: stream synchronisation failed");
+    rc = PRIO3GPU_E_HIP;
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../include/prio3gpu.h"
+#include "../../include/prio3gpu_test.h"
 
 namespace {
 
@@ -583,11 +584,15 @@ __attribute__((target("avx512f,avx512ifma"))) void x25519_x8(uint8_t out[8][32],
   }
 }
 
-bool have_ifma() {
-  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512ifma") &&
-                         !getenv("PRIO3GPU_NO_IFMA");
+bool cpu_has_ifma() {
+  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512ifma");
   return ok;
 }
+
+// the 8-report ladder unless prio3gpu_test_hpke_set_ifma(0) switched it off (no environment read)
+std::atomic<int> g_use_ifma{1};
+
+bool have_ifma() { return cpu_has_ifma() && g_use_ifma.load(std::memory_order_relaxed) != 0; }
 
 bool x25519_dh(const uint8_t* sk, const uint8_t* pk, uint8_t* dh) {
   x25519(dh, sk, pk);
@@ -954,6 +959,11 @@ int prio3gpu_hpke_open_report_shares(const uint8_t* task_id, const prio3gpu_hpke
     for (size_t i = b; i < e; ++i) open_i(i, pre[i - b] ? dh8[i - b] : nullptr);
   });
   return 0;
+}
+
+int prio3gpu_test_hpke_set_ifma(int on) {
+  if (on && !cpu_has_ifma()) return PRIO3GPU_E_UNSUPPORTED;
+  return g_use_ifma.exchange(on ? 1 : 0);
 }
 
 }  // extern "C"

@@ -1090,6 +1090,15 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
   pt_out = pt;
 }
 
+// The paired Sum query's shape (calls = m/2, Field128; sum_query_pair): the launch gives the
+// kernel its LDS-DMA windows (4 waves x kSqWin of dynamic LDS) only then, so the other shapes
+// (e.g. sum5) keep the CU's LDS for more blocks.
+__host__ __device__ inline bool flpq_pair(const Cfg& cfg) {
+  return cfg.es == 16 && cfg.kind == KIND_SUM && 2u * cfg.calls == cfg.m && cfg.m >= 8u &&
+         cfg.arity == 1u;
+}
+constexpr uint32_t kFlpqPairLds = 4u * kSqWin;  // per 256-thread block
+
 #ifndef FLPQ_WAVES  // at least 2 waves/SIMD (<= 256 VGPRs) for the Field128 paired Sum query
 #define FLPQ_WAVES __attribute__((amdgpu_waves_per_eu(2)))
 #endif
@@ -1133,8 +1142,7 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
   // Sum with calls = m/2 (Field128): the paired query, whole waves (its operands arrive by
   // LDS-DMA for all 64 lanes); every other shape: one independent lane per live report
   bool pair = false;
-  if constexpr (FO::ES == 16)
-    pair = cfg.kind == KIND_SUM && 2u * cfg.calls == cfg.m && cfg.m >= 8u && cfg.arity == 1u;
+  if constexpr (FO::ES == 16) pair = flpq_pair(cfg);
   if (!pair && !live) return;
   const uint32_t lane = threadIdx.x & 63u, r0w = r - lane;
   if (pair && r0w >= n) return;  // wave-uniform
@@ -1178,7 +1186,7 @@ __global__ void __launch_bounds__(256) FLPQ_WAVES k_flp_query_lane(Cfg cfg, uint
   bad |= !FO::is_canonical(s0) || !FO::is_canonical(s1);
   if constexpr (FO::ES == 16) {
     if (pair) {
-      __shared__ __attribute__((aligned(16))) uint8_t sqlds[4 * kSqWin];
+      extern __shared__ __attribute__((aligned(16))) uint8_t sqlds[];  // kFlpqPairLds
       const bool r_root = FO::eq(rmm, one);  // y_i = 1 for some i: the generic loop below
       bool pbad = bad;
       T pt, w0, v;
@@ -2441,6 +2449,26 @@ __global__ void __launch_bounds__(256) k_merge_ranks(uint8_t* dst, const uint8_t
       m.tmax = x.tmax > m.tmax ? x.tmax : m.tmax;
     }
     meta[s] = m;
+  }
+}
+
+// Epoch merge staging (prio3gpu_agg_epoch_merge): local slot s (blockIdx.y) is copied to the
+// union table's slot map[s] -- share row (8-byte words), count, slot meta -- of a staging
+// aggregate that starts empty; union slots no local slot maps to stay empty.
+__global__ void __launch_bounds__(256) k_agg_scatter(uint64_t* dst_share,
+                                                     unsigned long long* dst_counts,
+                                                     SlotMeta* dst_meta, const uint64_t* src_share,
+                                                     const unsigned long long* src_counts,
+                                                     const SlotMeta* src_meta, const uint32_t* map,
+                                                     size_t row_words) {
+  const uint32_t s = blockIdx.y, d = map[s];
+  if (d == 0xFFFFFFFFu) return;  // PRIO3GPU_SLOT_UNUSED: a pooled slot no job of the epoch used
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < row_words;
+       i += (size_t)gridDim.x * blockDim.x)
+    dst_share[(size_t)d * row_words + i] = src_share[(size_t)s * row_words + i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    dst_counts[d] = src_counts[s];
+    dst_meta[d] = src_meta[s];
   }
 }
 

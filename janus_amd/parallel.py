@@ -1,8 +1,16 @@
 """Report sharding across GPUs: one process per GPU, contiguous report ranges,
-no data-path collective; the only exchange is the end-of-job merge of per-GPU partial aggregate
-shares (RCCL all-gather of raw LE field-element bytes + mod-p add kernel, `Comm.allreduce`) with
-the checksum / interval half of `BatchAggregation::merged_with` folded on the host
-(`merge_batch_aggregations`, the same C-ABI function the GPU merge calls).
+no data-path collective; the only exchange is the merge of per-GPU partial aggregate shares (RCCL
+all-gather of raw LE field-element bytes + mod-p add kernel) with the checksum / interval half of
+`BatchAggregation::merged_with`.
+
+Two merge contracts:
+  * per job, `Comm.allreduce` (prio3gpu_agg_allreduce): every rank flushes every job in lockstep
+    (the bench's step, one job per rank per step);
+  * per epoch, `EpochPartials` (host) / `epoch_merge_device` (prio3gpu_agg_epoch_merge): each
+    rank keeps its partials across ANY number of independent jobs, keyed by batch identifier, and
+    the ranks merge once at an epoch boundary (a collection), every rank calling the merge for
+    epochs in the same order -- the shape Janus's independent job drivers can run
+    (binary_utils/job_driver.rs:119-216) and the shard merge of aggregate_share.rs:44-66.
 
 Janus analogue: independent aggregation jobs on concurrent job-driver workers
 (`aggregator/src/binary_utils/job_driver.rs:119-216`) whose partial batch aggregations are merged
@@ -66,3 +74,62 @@ def merge_batch_aggregations(field_size: int, parts: Iterable[BatchAggregation])
                                                  ctypes.byref(src)), "batch aggregation merge")
     return BatchAggregation(acc_buf.raw[:n * field_size], acc.report_count, bytes(acc.checksum),
                             (acc.interval_start, acc.interval_duration))
+
+
+def epoch_union(epoch: int, local_keys, all_gather):
+    """The epoch's union slot table: the sorted union of every rank's batch identifiers, agreed
+    over the host channel `all_gather(obj) -> [obj of each rank]` (e.g.
+    torch.distributed.all_gather_object).  Every rank must be at the same epoch."""
+    got = all_gather((epoch, sorted(bytes(k) for k in local_keys)))
+    epochs = sorted(set(e for e, _ in got))
+    if len(epochs) != 1:
+        raise RuntimeError(f"epoch merge: ranks are at epochs {epochs}")
+    return sorted(set().union(*(set(k) for _, k in got)))
+
+
+class EpochPartials:
+    """One rank's partial `BatchAggregation`s, kept across any number of aggregation jobs and
+    keyed by batch identifier (bytes), merged across ranks once per epoch (host path: the
+    prio3gpu_batch_aggregation_merge fold; the device path is `epoch_merge_device`)."""
+
+    def __init__(self, field_size: int):
+        self.field_size = field_size
+        self.parts = {}
+        self.epoch = 0
+
+    def add(self, key: bytes, ba: BatchAggregation):
+        """Accumulator::update_aggregated of one job's slot into this rank's partial."""
+        key = bytes(key)
+        cur = self.parts.get(key)
+        self.parts[key] = ba if cur is None else merge_batch_aggregations(self.field_size,
+                                                                          [cur, ba])
+
+    def merge_epoch(self, all_gather):
+        """The epoch's merged aggregations on every rank ({key: BatchAggregation}, each key
+        folded over the ranks that hold it, in rank order); the partials are reset and the
+        epoch advances."""
+        got = all_gather((self.epoch, self.parts))
+        epochs = sorted(set(e for e, _ in got))
+        if len(epochs) != 1:
+            raise RuntimeError(f"epoch merge: ranks are at epochs {epochs}")
+        union = sorted(set().union(*(set(p) for _, p in got)))
+        out = {k: merge_batch_aggregations(self.field_size, [p[k] for _, p in got if k in p])
+               for k in union}
+        self.parts = {}
+        self.epoch += 1
+        return out
+
+
+def epoch_merge_device(comm, vdaf, local, local_keys, epoch: int, all_gather):
+    """prio3gpu_agg_epoch_merge over a device partial `local` (AggregateShares whose slot i holds
+    batch identifier local_keys[i]; slots past len(local_keys) unused): returns (union keys,
+    AggregateShares of the merged totals, one slot per union key).  Every rank calls it once per
+    epoch, epochs in the same order."""
+    from .prio3 import SLOT_UNUSED
+    union = epoch_union(epoch, local_keys, all_gather)
+    idx = {k: i for i, k in enumerate(union)}
+    slot_map = [idx[bytes(k)] for k in local_keys]
+    slot_map += [SLOT_UNUSED] * (local.num_slots - len(slot_map))
+    total = vdaf.new_aggregate(len(union))
+    comm.epoch_merge(vdaf, local, slot_map, total)
+    return union, total

@@ -31,6 +31,7 @@ COUNT, SUM, SUMVEC, HISTOGRAM, FPVEC = 0, 1, 2, 3, 4
 # 0.6, the default); XofTurboShake128 = draft-irtf-cfrg-vdaf-08+ (forward compatibility, parity
 # unpinned)
 XOF_SHAKE128, XOF_TURBOSHAKE128 = 0, 1
+SLOT_UNUSED = 0xFFFFFFFF  # PRIO3GPU_SLOT_UNUSED (prio3gpu_agg_epoch_merge)
 STATUS_OK, STATUS_VDAF_PREP_ERROR, STATUS_INVALID_MESSAGE = 0, 5, 8
 
 FIELD64_MODULUS = 2**64 - 2**32 + 1
@@ -529,6 +530,17 @@ class Comm:
         check(lib().prio3gpu_agg_allreduce(self._h, vdaf._ctx, local._h,
                                            total._h if total is not None else None),
               "agg_allreduce")
+
+    def epoch_merge(self, vdaf: Prio3Gpu, local: AggregateShares, slot_map,
+                    total: AggregateShares):
+        """prio3gpu_agg_epoch_merge: total[slot_map[s]] += sum over ranks of local[s] (one entry
+        per local slot; SLOT_UNUSED for a slot the epoch's jobs did not use), local reset.  A
+        collective: every rank, once per epoch, epochs in the same order."""
+        m = np.ascontiguousarray(slot_map, dtype=np.uint32)
+        if m.shape != (local.num_slots,):
+            raise ValueError(f"slot_map needs {local.num_slots} entries, got {m.shape}")
+        check(lib().prio3gpu_agg_epoch_merge(self._h, vdaf._ctx, local._h, _ptr(m),
+                                             total.num_slots, total._h), "agg_epoch_merge")
 
     def close(self):
         if getattr(self, "_h", None):

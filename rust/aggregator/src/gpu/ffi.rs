@@ -39,6 +39,7 @@ pub const PRIO3GPU_E_INVALID_MESSAGE: c_int = -7;
 
 pub const PRIO3GPU_XOF_SHAKE128: c_int = 0;
 pub const PRIO3GPU_XOF_TURBOSHAKE128: c_int = 1;
+pub const PRIO3GPU_SLOT_UNUSED: u32 = 0xFFFF_FFFF;
 
 // ---- opaque handles --------------------------------------------------------------------------
 #[repr(C)]
@@ -219,23 +220,15 @@ extern "C" {
     pub fn prio3gpu_comm_destroy(comm: *mut prio3gpu_comm) -> c_int;
     pub fn prio3gpu_agg_allreduce(comm: *mut prio3gpu_comm, ctx: *mut prio3gpu_ctx,
                                   local: *mut prio3gpu_agg, total: *mut prio3gpu_agg) -> c_int;
+    pub fn prio3gpu_agg_epoch_merge(comm: *mut prio3gpu_comm, ctx: *mut prio3gpu_ctx,
+                                    local: *mut prio3gpu_agg, slot_map: *const u32,
+                                    union_slots: u32, total: *mut prio3gpu_agg) -> c_int;
 
-    // -- profiling, tests, device memory ------------------------------------------------------
+    // -- profiling (the test hooks of include/prio3gpu_test.h are not bound) -------------------
     pub fn prio3gpu_prof_enable(ctx: *mut prio3gpu_ctx, on: c_int) -> c_int;
     pub fn prio3gpu_prof_read(ctx: *mut prio3gpu_ctx, ms: *mut f64, launches: *mut u64,
                               max_kernels: c_int) -> c_int;
     pub fn prio3gpu_prof_kernel_name(kernel_id: c_int) -> *const c_char;
-    pub fn prio3gpu_test_squeeze(field_size: c_int, blocks: *const u64, nblocks: usize, n: u32,
-                                 out: *mut u8, exact: c_int) -> c_int;
-    pub fn prio3gpu_test_flp_query(ctx: *mut prio3gpu_ctx, n: usize,
-                                   leader_input_shares: *const u8, query_rand: *const u8,
-                                   joint_rand: *const u8, own_parts: *const u8,
-                                   out_prep_shares: *mut u8, status: *mut u8) -> c_int;
-    pub fn prio3gpu_dev_alloc(ctx: *mut prio3gpu_ctx, bytes: usize, out: *mut *mut c_void)
-                              -> c_int;
-    pub fn prio3gpu_dev_free(ctx: *mut prio3gpu_ctx, p: *mut c_void) -> c_int;
-    pub fn prio3gpu_memcpy(ctx: *mut prio3gpu_ctx, dst: *mut c_void, src: *const c_void,
-                           bytes: usize) -> c_int;
 
     // -- DAP codec edge (host) ----------------------------------------------------------------
     pub fn prio3gpu_decode_agg_init_req(msg: *const u8, len: usize, query_type: c_int,

@@ -723,10 +723,37 @@ impl GpuComm {
     }
 
     /// total += sum over ranks of `local` (mod p, counts, checksum XOR, interval union); `local`
-    /// is reset.  Every rank calls it with the same slot count, in the same order.
+    /// is reset.  Every rank calls it with the same slot count, in the same order: a per-job
+    /// lockstep flush, only for drivers that step jobs in lockstep across GPUs.
     pub fn allreduce(&self, engine: &GpuPrio3, local: &mut AggregateShares,
                      total: &mut AggregateShares) -> Result<(), GpuError> {
         check(unsafe { ffi::prio3gpu_agg_allreduce(self.comm, engine.ctx, local.agg, total.agg) })
+    }
+
+    /// The epoch merge for independent job drivers (prio3gpu_agg_epoch_merge): `local` is this
+    /// GPU's partial over any number of jobs, its slot i holding batch identifier `keys[i]`;
+    /// `union` is the epoch's sorted union of every rank's keys (agreed over the host channel,
+    /// identical on every rank).  Returns the totals, one slot per union key; `local` is reset.
+    /// Every rank calls it once per epoch, epochs in the same order, one merger per communicator.
+    pub fn epoch_merge<K: Eq + Hash>(&self, engine: &GpuPrio3, local: &mut AggregateShares,
+                                     keys: &[K], union: &[K])
+                                     -> Result<AggregateShares, GpuError> {
+        let index: HashMap<&K, u32> = union.iter().enumerate().map(|(i, k)| (k, i as u32)).collect();
+        let mut slot_map = vec![ffi::PRIO3GPU_SLOT_UNUSED; local.slots as usize];
+        if keys.len() > slot_map.len() {
+            return Err(arg_error("epoch merge: more keys than local slots".into()));
+        }
+        for (s, k) in keys.iter().enumerate() {
+            slot_map[s] = *index
+                .get(k)
+                .ok_or_else(|| arg_error("epoch merge: a local key is not in the union".into()))?;
+        }
+        let mut total = engine.new_aggregate(union.len() as u32)?;
+        check(unsafe {
+            ffi::prio3gpu_agg_epoch_merge(self.comm, engine.ctx, local.agg, slot_map.as_ptr(),
+                                          union.len() as u32, total.agg)
+        })?;
+        Ok(total)
     }
 }
 

@@ -284,6 +284,49 @@ def test_rccl_merge_single_rank():
     comm.close()
 
 
+def test_rccl_epoch_merge_remaps_slots():
+    """prio3gpu_agg_epoch_merge with one rank: two jobs accumulate into ONE pooled partial whose
+    slots hold batch identifiers in first-seen order (k2, k0, k5; slot 3 unused); the epoch merge
+    lands each slot in the union table (k0, k1, k2, k5; k1 seen only by another rank) -- shares,
+    counts, checksums and intervals -- and resets the partial.  Reference: the batch-aggregation
+    shard merge, aggregate_share.rs:44-66."""
+    from janus_amd.parallel import epoch_merge_device
+    from janus_amd.prio3 import Comm
+    b = batch("hist4")
+    v = gpu_vdaf(b)
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    h = b.n // 2
+    keys = [b"k2", b"k0", b"k5"]
+    # report -> local slot: job A (first half) sees k2, k0; job B sees k0, k5
+    slots = np.array([(r % 2) if r < h else 1 + (r % 2) for r in range(b.n)], np.uint32)
+    times = np.arange(500, 500 + b.n, dtype=np.uint64)
+    local = v.new_aggregate(4)
+    for lo, hi in ((0, h), (h, b.n)):  # two independent jobs, no collective between them
+        ls = v.new_state(0, hi - lo)
+        _, lst = v.prepare_init(ls, b.nonces[lo:hi], b.public[lo:hi], b.leader_in[lo:hi])
+        v.prepare_next(ls, b.prep_msg[lo:hi], lst, want_output_shares=False, agg=local,
+                       batch_slots=slots[lo:hi])
+        local.update_reports(b.nonces[lo:hi], times[lo:hi], lst, slots[lo:hi])
+        ls.close()
+    before = [(local.read(s), local.read_reports(s)) for s in range(3)]
+    union, total = epoch_merge_device(comm, v, local, keys, 0,
+                                      lambda obj: [obj, (0, [b"k1"])])
+    assert union == [b"k0", b"k1", b"k2", b"k5"]
+    for s, k in enumerate(keys):
+        u = union.index(k)
+        assert (total.read(u), total.read_reports(u)) == before[s]
+        want, cnt = expected_aggregate(b, "leader", slots=slots, slot=s)
+        assert total.read(u) == (want, cnt) and cnt > 0
+    assert total.read(union.index(b"k1"))[1] == 0  # another rank's key: empty here
+    assert all(local.read(s)[1] == 0 for s in range(4))
+    assert local.read_reports(0) == (bytes(32), (0, 0))
+    with pytest.raises(Exception):  # a slot map that sends two slots to one union slot
+        comm.epoch_merge(v, local, [0, 0, 1, 2], v.new_aggregate(3))
+    total.close()
+    local.close()
+    comm.close()
+
+
 @pytest.mark.parametrize("name", list(SIZES))
 def test_gpu_shard_matches_oracle(name):
     """Client::shard + FLP prove on the GPU reproduce the oracle's public/leader/helper shares."""

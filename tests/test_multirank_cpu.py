@@ -132,3 +132,95 @@ def test_shard_ranges_cover():
             rs = [shard_range(n, w, r) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+
+
+# ---- epoch merge: independent job counts per rank, one merge per epoch -------------------------
+# Reports r = 0..N_EPOCH-1 arrive in jobs of JOB reports; rank 0 drives 3 jobs, rank 1 drives 5
+# (independent job drivers: no per-job collective).  Report r falls in batch identifier
+# r // BUCKET (time-interval buckets), so the ranks hold different key sets.
+N_EPOCH, JOB, BUCKET = 40, 5, 7
+JOBS_OF = {0: [0, 1, 2], 1: [3, 4, 5, 6, 7]}
+
+
+def _key_partials(reports):
+    """{key: (leader, helper) BatchAggregation} of the given report indices, per batch
+    identifier, from the C restatement."""
+    from janus_amd.parallel import BatchAggregation
+    from oracle import prio3 as O
+    from oracle.ref import Prio3Ref
+    from tests.reports import CONFIGS
+    c = CONFIGS[NAME]
+    r = Prio3Ref(c["kind"], O.synth_verify_key(b"ep"), c["bits"], c["length"], c["chunk"])
+    g = r.gen(b"ep", 0, N_EPOCH, threads=1)
+    out = {}
+    for key in sorted(set(i // BUCKET for i in reports)):
+        idx = [i for i in reports if i // BUCKET == key]
+        res = r.prepare_batch(g["nonces"][idx], g["public"][idx], g["leader_in"][idx],
+                              g["helper_in"][idx], threads=1, outputs=False)
+        t = [T0 + 37 * i for i in idx]
+        iv = (min(t), max(t) - min(t) + 1)
+        ck = _checksum(g["nonces"][idx])
+        out[key.to_bytes(4, "big")] = tuple(BatchAggregation(res[k].tobytes(), res["count"], ck, iv)
+                                            for k in ("agg_l", "agg_h"))
+    return out
+
+
+def _epoch_rank_main(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from janus_amd.parallel import EpochPartials
+
+    def all_gather(obj):
+        got = [None] * world
+        dist.all_gather_object(got, obj)
+        return got
+    parts = [EpochPartials(16), EpochPartials(16)]  # leader, helper
+    for job in JOBS_OF[rank]:  # each job flushes into this rank's partials, no collective
+        for key, bas in _key_partials(range(job * JOB, (job + 1) * JOB)).items():
+            for which in (0, 1):
+                parts[which].add(key, bas[which])
+    merged = [p.merge_epoch(all_gather) for p in parts]
+    # a second, empty epoch: the partials were reset and the epochs advance together
+    empty = [p.merge_epoch(all_gather) for p in parts]
+    q.put((rank, merged, empty, [p.epoch for p in parts]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_epoch_merge_different_job_counts():
+    """Ranks drive 3 and 5 jobs, keep per-key partials across their jobs and merge ONCE at the
+    epoch boundary: every rank's merged BatchAggregations (share, count, checksum, interval) equal
+    the single-process aggregation of all 40 reports per batch identifier, bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_epoch_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p_ in procs:
+        p_.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=180) for _ in procs))
+    for p_ in procs:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    want = _key_partials(range(N_EPOCH))
+    assert len(want) == -(-N_EPOCH // BUCKET)
+    for rank in (0, 1):
+        merged, empty, epochs = got[rank]
+        assert epochs == [2, 2] and empty == [{}, {}]
+        for which in (0, 1):
+            assert sorted(merged[which]) == sorted(want)
+            for key, w in want.items():
+                g = merged[which][key]
+                assert g.aggregate_share == w[which].aggregate_share
+                assert g.report_count == w[which].report_count
+                assert g.checksum == w[which].checksum and g.interval == w[which].interval
+
+
+def test_epoch_merge_refuses_ranks_at_different_epochs():
+    from janus_amd.parallel import EpochPartials, epoch_union
+    p = EpochPartials(16)
+    with pytest.raises(RuntimeError):
+        p.merge_epoch(lambda obj: [obj, (obj[0] + 1, {})])
+    with pytest.raises(RuntimeError):
+        epoch_union(3, [b"a"], lambda obj: [obj, (2, [b"b"])])
+    assert epoch_union(3, [b"b", b"a"], lambda obj: [obj, (3, [b"c", b"a"])]) == [b"a", b"b", b"c"]
