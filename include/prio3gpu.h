@@ -139,6 +139,12 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
  *   "wires_mfma"    1: SumVec (chunk > 64) wire pass on the matrix cores; 0: VALU k_flp_wires
  *   "wires_cols"    1: chunk <= 64 lane-per-column wire pass; 0: VALU k_flp_wires
  *   "fused_helper"  1: FixedPoint helper XOF pipeline (k_helper_xof); 0: exact two-pass path
+ *   "helper_snap"   1: FixedPoint helper states (created after the call) keep 200-B sponge
+ *                   snapshots of every 64th block instead of the expanded measurement share
+ *                   (1/54 of its HBM); its rows are regenerated per chunk where they are read
+ *                   (FLP query, accumulation past the column sums, output shares); 0: full rows
+ *   "snap_chunk"    reports per FixedPoint query / regeneration chunk (default 512; the
+ *                   regenerated rows of one chunk are the only full-size helper scratch)
  *   "jr_ring"       1: FixedPoint leader joint-rand part via k_jr_ring; 0: k_jr
  *   "spread"        1: latency-bound sponge launches take one CU per workgroup
  *   "expand_lds", "jr_lds"  dynamic LDS bytes per k_expand / k_jr block (0 = none): caps those

@@ -148,7 +148,7 @@ enum KernelId {
   KID_PNEXT, KID_ACC_PART, KID_ACC_SPEC, KID_ACC_MERGE, KID_OUT, KID_MERGE, KID_SHARD_SEEDS,
   KID_SHARD_MEAS, KID_SHARD_JR, KID_PROVE, KID_SHARD_PROOF, KID_REPORT_META, KID_REPORT_META_FOLD,
   KID_SHARD_NORM, KID_JR_RING, KID_FLP_QUERY_LANE, KID_FLP_WIRES_COLS, KID_FLP_WIRES_MFMA,
-  KID_COUNT
+  KID_FPV_REGEN, KID_COUNT
 };
 const char* const kKernelNames[KID_COUNT] = {
     "k_query_rand", "k_expand", "k_helper_xof", "k_jr", "k_flp_weights", "k_flp_wires",
@@ -156,7 +156,7 @@ const char* const kKernelNames[KID_COUNT] = {
     "k_prepare_next", "k_accum_partial", "k_accum_spec", "k_accum_merge", "k_out_shares", "k_merge",
     "k_shard_seeds", "k_shard_meas", "k_shard_jr", "k_flp_prove", "k_shard_proof", "k_report_meta",
     "k_report_meta_fold", "k_shard_norm", "k_jr_ring", "k_flp_query_lane", "k_flp_wires_cols",
-    "k_flp_wires_mfma"};
+    "k_flp_wires_mfma", "k_fpv_regen"};
 
 // Per-kernel HIP-event timing on the context's stream (opt-in; used by bench.py).
 struct Prof {
@@ -196,6 +196,10 @@ struct prio3gpu_ctx {
   // measured-fastest paths; every alternative is parity-tested against the oracle.
   bool speculate = true;     // "speculate": accumulation from k_jr's column sums (0: direct)
   bool fused_helper = true;  // "fused_helper": FixedPoint helper via k_helper_xof (0: two-pass)
+  // "helper_snap": FixedPoint helper states keep sponge snapshots instead of the expanded share
+  // (k_fpv_regen rewrites it per chunk); read when a state is created
+  bool helper_snap = true;
+  uint32_t snap_chunk = 512;  // "snap_chunk": reports per FixedPoint query / regeneration chunk
   bool spread = true;        // "spread": one CU per workgroup for latency-bound sponge launches
   bool jr_ring = true;       // "jr_ring": FixedPoint leader joint-rand part via k_jr_ring
   bool wires_mfma = true;    // "wires_mfma": SumVec chunk > 64 wire pass on the matrix cores
@@ -255,6 +259,13 @@ struct prio3gpu_state {
   size_t in_pitch = 0;  // row pitch of the caller's input shares (0: packed, the share length)
   DevBuf t, jr, part, seed, meas, proof, prep, msg, status, nonces, pub, input, w;
   DevBuf fpart, flags;  // FixedPointBoundedL2VecSum: wire partials per row group, query flags
+  size_t fpart_rows = 0;  // reports fpart holds (the query runs in chunks of at most this many)
+  // FixedPoint helper, snapshot mode (helper_snap): k_helper_xof's sponge snapshots of every
+  // report; `scratch` holds one chunk of regenerated measurement-share rows.  snap_active: the
+  // prepared batch's share exists only as snapshots (the fused path ran), so every reader of
+  // meas_rows goes through regen_rows.
+  DevBuf snaps, scratch;
+  bool snap = false, snap_active = false;
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
   CRows proof_rows{nullptr, 0};  // proof shares (prepare_init_xof -> prepare_init_query)
   bool xof_done = false;         // the XOF phase ran; the query phase is due
@@ -547,22 +558,45 @@ bool spec_range(const Cfg& g, uint32_t& nd, uint32_t& e0, uint32_t& e1) {
   return e1 > e0;
 }
 
-// FixedPointBoundedL2VecSum FLP query (fpvec_kernels.h): weights, wire passes, finalize.
-int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, CRows proof,
-                     uint8_t* d_status) {
+// Snapshot mode: the helper's expanded measurement shares of reports [r0, r0 + nr) rewritten
+// from k_helper_xof's sponge snapshots into st->scratch rows 0..nr-1 (k_fpv_regen).
+int regen_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t nr) {
+  const Cfg& g = c->cfg;
+  const size_t row = (size_t)g.meas_len * g.es;
+  CHK(st->scratch.ensure(nr * row));
+  const uint64_t lanes = (uint64_t)nr * snap_count(g);
+  PROF(KID_FPV_REGEN);
+  hipLaunchKernelGGL(k_fpv_regen, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, c->stream, g,
+                     (uint32_t)nr, (uint32_t)r0, reinterpret_cast<const uint64_t*>(st->snaps.p),
+                     Rows{st->scratch.u8(), row});
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// Reports per FixedPoint query / regeneration chunk.
+size_t fpv_chunk(const prio3gpu_ctx* c, const prio3gpu_state* st, size_t n) {
+  return std::max<size_t>(1, std::min<size_t>({n, (size_t)c->snap_chunk, st->fpart_rows}));
+}
+
+// FixedPointBoundedL2VecSum FLP query (fpvec_kernels.h): weights, wire passes, finalize, over
+// reports [r0, r0 + n) (rows 0..n-1 of `meas` and `proof`; the state's per-report arrays at r0).
+int launch_fpv_query_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t n, CRows meas,
+                          CRows proof, uint8_t* d_status) {
   const Cfg& g = c->cfg;
   const uint32_t N = (uint32_t)n;
   const uint32_t H = fpv_rows(g);
   const FpvW W = fpv_w_layout(g);
-  Rows wrows{st->w.u8(), (size_t)W.len * 16};
-  Rows prep{st->prep.u8(), g.prep_share_len};
-  uint32_t* flags = reinterpret_cast<uint32_t*>(st->flags.p);
+  Rows wrows{st->w.u8() + r0 * (size_t)W.len * 16, (size_t)W.len * 16};
+  Rows prep{st->prep.u8() + r0 * g.prep_share_len, g.prep_share_len};
+  uint32_t* flags = reinterpret_cast<uint32_t*>(st->flags.p) + r0;
+  const CRows tq{st->t.u8() + r0 * 32, 32}, jr{st->jr.u8() + r0 * 32, 32};
+  const CRows part{st->part.u8() + r0 * 16, 16};
   HIPCHK(hipMemsetAsync(flags, 0, n * 4, c->stream));
   const size_t lds = (size_t)16 * (3 * (size_t)g.m + g.chunk + 1 + 12) + 16;
   {
     PROF(KID_FPV_WEIGHTS);
-    hipLaunchKernelGGL(k_fpv_weights, dim3(N, 2), dim3(256), lds, c->stream, g, N, proof,
-                       CRows{st->t.u8(), 32}, CRows{st->jr.u8(), 32}, prep, d_status, wrows, flags);
+    hipLaunchKernelGGL(k_fpv_weights, dim3(N, 2), dim3(256), lds, c->stream, g, N, proof, tq, jr,
+                       prep, d_status, wrows, flags);
   }
   {
     PROF(KID_FPV_WIRES0);
@@ -578,10 +612,29 @@ int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, 
   {
     PROF(KID_FPV_FINAL);
     hipLaunchKernelGGL(k_fpv_finalize, dim3((g.chunk + 255) / 256, N), dim3(256), 0, c->stream, g,
-                       N, H, meas, CRows{wrows.base, wrows.stride}, CRows{st->jr.u8(), 32},
-                       CRows{st->part.u8(), 16}, st->fpart.u8(), prep, d_status, flags);
+                       N, H, meas, CRows{wrows.base, wrows.stride}, jr, part, st->fpart.u8(), prep,
+                       d_status, flags);
   }
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// The query over the whole batch in chunks of fpv_chunk reports (the wire partials `fpart` hold
+// one chunk); a snapshot-mode helper batch regenerates each chunk's shares first.
+int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, CRows proof,
+                     uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  const size_t ch = fpv_chunk(c, st, n);
+  for (size_t r0 = 0; r0 < n; r0 += ch) {
+    const size_t nr = std::min(ch, n - r0);
+    CRows m{meas.base + r0 * meas.stride, meas.stride};
+    if (st->snap_active) {
+      CHK(regen_rows(c, st, r0, nr));
+      m = CRows{st->scratch.u8(), (size_t)g.meas_len * g.es};
+    }
+    CHK(launch_fpv_query_rows(c, st, r0, nr, m, CRows{proof.base + r0 * proof.stride, proof.stride},
+                              d_status + r0));
+  }
   return 0;
 }
 
@@ -688,7 +741,8 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
                              CRows{d_in, in_pitch}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
                              Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb,
-                             spec_lo, spec_cy);
+                             spec_lo, spec_cy,
+                             st->snap ? reinterpret_cast<uint64_t*>(st->snaps.p) : nullptr);
         }
         uint32_t h_fb = 0;
         HIPCHK(hipMemcpyAsync(&h_fb, fb, 4, hipMemcpyDeviceToHost, c->stream));
@@ -697,12 +751,24 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
       }
     }
     if (fused_done) {  // the storer wave wrote the speculative column sums
+      st->snap_active = st->snap;
+      if (st->snap_active && st->spec_ok) {
+        // the storer summed EVERY word of the share: the column sums cover all elements, so no
+        // edge element is read from rows that only exist as snapshots
+        st->spec_e0 = 0;
+        st->spec_e1 = g.meas_len;
+      }
       st->meas_rows = CRows{mo.base, mo.stride};
       st->proof_rows = CRows{po.base, po.stride};
       st->n = n;
       st->xof_done = true;
       st->weights_done = false;
       return 0;
+    }
+    st->snap_active = false;
+    if (st->snap) {  // the exact path (non-canonical element, or fused path off) stores the rows
+      CHK(st->meas.ensure(n * (size_t)g.meas_len * es));
+      mo = Rows{st->meas.u8(), (size_t)g.meas_len * es};
     }
     {
       PROF(KID_EXPAND);
@@ -1056,7 +1122,9 @@ int launch_accumulate(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint3
     const uint32_t e0 = st->spec_e0, e1 = st->spec_e1;
     const uint32_t nedge = e0 + (g.meas_len - e1);
     const uint32_t epb_e = std::min<uint32_t>(256, std::max<uint32_t>(1, nedge));
-    const uint32_t tiles_e = (nedge + epb_e - 1) / epb_e;
+    // at least one tile: its first row of blocks also counts each chunk's accepted reports (a
+    // snapshot-mode batch has no edge elements -- its column sums cover every element)
+    const uint32_t tiles_e = std::max<uint32_t>(1, (nedge + epb_e - 1) / epb_e);
     {
       PROF(KID_ACC_PART);
       hipLaunchKernelGGL(k_accum_partial<FO>, dim3(nspec, tiles_e), dim3(256), red_lds, c->stream, g,
@@ -1095,6 +1163,61 @@ int launch_out_shares(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8
   }
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+// Accumulation of a prepared batch.  A snapshot-mode helper batch (its shares exist only as
+// snapshots) takes the speculative column sums as they are when they are exact without any row:
+// every report accepted, whole waves, one batch slot (the storer summed every element of every
+// row).  Otherwise its rows are regenerated chunk by chunk and summed directly.
+template <class FO>
+int accumulate_batch(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint32_t* slots,
+                     uint8_t* d_status, prio3gpu_agg* agg) {
+  if (!st->snap_active) return launch_accumulate<FO>(c, st, n, slots, d_status, agg);
+  const Cfg& g = c->cfg;
+  bool whole = st->spec_ok && st->spec_n == n && !slots && n % 64 == 0;
+  if (whole) {
+    std::vector<uint8_t> hs(n);
+    HIPCHK(hipMemcpyAsync(hs.data(), d_status, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (size_t r = 0; r < n && whole; ++r) whole = hs[r] == 0;
+  }
+  if (whole) return launch_accumulate<FO>(c, st, n, nullptr, d_status, agg);
+  const bool spec = st->spec_ok;
+  const CRows rows = st->meas_rows;
+  st->spec_ok = false;
+  const size_t ch = fpv_chunk(c, st, n);
+  int rc = 0;
+  for (size_t r0 = 0; r0 < n && rc == 0; r0 += ch) {
+    const size_t nr = std::min(ch, n - r0);
+    rc = regen_rows(c, st, r0, nr);
+    st->meas_rows = CRows{st->scratch.u8(), (size_t)g.meas_len * g.es};
+    if (rc == 0)
+      rc = launch_accumulate<FO>(c, st, nr, slots ? slots + r0 : nullptr, d_status + r0, agg);
+    // the next chunk's regeneration overwrites the scratch rows only after this chunk's sums
+    // (same stream)
+  }
+  st->spec_ok = spec;
+  st->meas_rows = rows;
+  return rc;
+}
+
+// Output shares of a prepared batch (a snapshot-mode helper batch: regenerated chunk by chunk).
+template <class FO>
+int out_shares_batch(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d_status,
+                     uint8_t* d_out) {
+  if (!st->snap_active) return launch_out_shares<FO>(c, st, n, d_status, d_out);
+  const Cfg& g = c->cfg;
+  const CRows rows = st->meas_rows;
+  const size_t ch = fpv_chunk(c, st, n), out_row = (size_t)g.out_len * g.es;
+  int rc = 0;
+  for (size_t r0 = 0; r0 < n && rc == 0; r0 += ch) {
+    const size_t nr = std::min(ch, n - r0);
+    rc = regen_rows(c, st, r0, nr);
+    st->meas_rows = CRows{st->scratch.u8(), (size_t)g.meas_len * g.es};
+    if (rc == 0) rc = launch_out_shares<FO>(c, st, nr, d_status + r0, d_out + r0 * out_row);
+  }
+  st->meas_rows = rows;
+  return rc;
 }
 
 bool is_f64(const prio3gpu_ctx* c) { return c->cfg.es == 8; }
@@ -1267,11 +1390,16 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
     rc |= st->w.ensure(N * (size_t)(flp_w_len(g) + flp_scratch_len(g)) * g.es);  // rows + scratch
   if (g.kind == KIND_FPVEC) {
     rc |= st->w.ensure(N * (size_t)fpv_w_layout(g).len * 16);
-    rc |= st->fpart.ensure(N * (size_t)fpv_rows(g) * g.chunk * 32);
+    st->fpart_rows = std::min<size_t>(N, c->snap_chunk);
+    rc |= st->fpart.ensure(st->fpart_rows * (size_t)fpv_rows(g) * g.chunk * 32);
     rc |= st->flags.ensure(N * 4);
   }
+  st->snap = g.kind == KIND_FPVEC && agg_id == 1 && c->helper_snap;
   if (agg_id == 1) {
-    rc |= st->meas.ensure(N * (size_t)g.meas_len * g.es);
+    if (st->snap)  // the expanded shares live as snapshots; the full rows only on the exact path
+      rc |= st->snaps.ensure(N * (size_t)snap_count(g) * kSnapBytes);
+    else
+      rc |= st->meas.ensure(N * (size_t)g.meas_len * g.es);
     rc |= st->proof.ensure(N * (size_t)g.proof_len * g.es);
   }
   if (rc) {
@@ -1605,6 +1733,14 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
     c->speculate = on;
   } else if (k == "fused_helper") {
     c->fused_helper = on;
+  } else if (k == "helper_snap") {
+    c->helper_snap = on;
+  } else if (k == "snap_chunk") {
+    if (value < 1 || value > 65536) {
+      set_err("option snap_chunk: %lld is outside [1, 65536]", (long long)value);
+      return PRIO3GPU_E_ARG;
+    }
+    c->snap_chunk = (uint32_t)value;
   } else if (k == "spread") {
     c->spread = on;
   } else if (k == "jr_ring") {
@@ -1768,16 +1904,16 @@ int prio3gpu_prepare_next(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const u
       d_out = c->io[5].u8();
     }
     if (is_f64(c))
-      CHK(launch_out_shares<Field64Ops>(c, st, n, d_status, d_out));
+      CHK(out_shares_batch<Field64Ops>(c, st, n, d_status, d_out));
     else
-      CHK(launch_out_shares<Field128Ops>(c, st, n, d_status, d_out));
+      CHK(out_shares_batch<Field128Ops>(c, st, n, d_status, d_out));
     CHK(copy_out(c, out_output_shares, d_out, bytes));
   }
   if (agg) {
     if (is_f64(c))
-      CHK(launch_accumulate<Field64Ops>(c, st, n, batch_slots, d_status, agg));
+      CHK(accumulate_batch<Field64Ops>(c, st, n, batch_slots, d_status, agg));
     else
-      CHK(launch_accumulate<Field128Ops>(c, st, n, batch_slots, d_status, agg));
+      CHK(accumulate_batch<Field128Ops>(c, st, n, batch_slots, d_status, agg));
   }
   CHK(copy_out(c, status, d_status, n));
   return finish_call(c, {prep_msgs, status, out_output_shares, batch_slots});
@@ -1827,9 +1963,9 @@ int prio3gpu_helper_init(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const ui
   }
   if (agg) {
     if (f64)
-      CHK(launch_accumulate<Field64Ops>(c, st, n, batch_slots, d_status, agg));
+      CHK(accumulate_batch<Field64Ops>(c, st, n, batch_slots, d_status, agg));
     else
-      CHK(launch_accumulate<Field128Ops>(c, st, n, batch_slots, d_status, agg));
+      CHK(accumulate_batch<Field128Ops>(c, st, n, batch_slots, d_status, agg));
   }
   CHK(copy_out(c, out_prep_msgs, d_msg, n * g.prep_msg_len));
   CHK(copy_out(c, status, d_status, n));
@@ -1853,6 +1989,8 @@ int launch_shard(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t* d
   const uint32_t N = (uint32_t)n, es = g.es;
   const size_t rs = (size_t)prio3gpu_random_size(c);
   // scratch: helper meas/proof (state), proof + prove rand + jr (state buffers reused)
+  CHK(st->meas.ensure(n * (size_t)g.meas_len * es));  // a snapshot-mode state has no rows yet
+  st->snap_active = false;
   CHK(st->prep.ensure(n * (size_t)g.proof_len * es));       // full proof
   CHK(st->jr.ensure(n * (size_t)std::max<uint32_t>(g.prove_rand_len, 1) * es + n * 32));
   uint8_t* d_proof = st->prep.u8();

@@ -78,13 +78,27 @@ DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[1
 constexpr uint32_t kHxRows = 64;              // reports per workgroup (1 producer + 1 consumer wave)
 constexpr uint32_t kHxDepth = 4;              // ring slots: the producer may run 4 blocks ahead
 
+// Snapshot mode (engine option helper_snap, the default for FixedPoint vectors): instead of
+// storing the 25.6 MB expanded measurement share of every report (entries = 100k), the producer
+// keeps the 200-byte sponge state of every kSnapEvery-th block, and k_fpv_regen rewrites any
+// range of reports' shares from those snapshots -- in parallel over the snapshots, so the
+// rewrite is throughput-bound (a 64-permutation chain per lane), not a 152K-permutation chain.
+// The share then costs 200 B per 10.75 KB (1/54) in HBM and twice as many reports fit in flight.
+constexpr uint32_t kSnapEvery = 64;  // producer blocks per state snapshot
+__host__ __device__ inline uint32_t snap_count(const Cfg& g) {
+  const uint32_t nprod = (2u * g.meas_len + 20u) / 21u;
+  return (nprod + kSnapEvery - 1u) / kSnapEvery;
+}
+constexpr size_t kSnapBytes = 25 * 8;  // one Keccak state
+
 template <uint32_t kDepth>
 __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
                                                     CRows nonces, CRows public_shares,
                                                     Rows out_meas, Rows out_proof, Rows out_part,
                                                     Rows out_seed, Rows out_jr,
                                                     const uint8_t* status, uint32_t* fallback,
-                                                    uint64_t* spec_lo, uint8_t* spec_cy) {
+                                                    uint64_t* spec_lo, uint8_t* spec_cy,
+                                                    uint64_t* snaps) {
   using FO = Field128Ops;
   // slot rows are kHxRows + 1 words apart: the storer's column reads (words x rows) hit distinct
   // banks; the producer's and consumer's row accesses stay conflict-free
@@ -146,6 +160,11 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
     bool perm = true;
     if (producer) {
       const int64_t j0 = 21 * i;
+      if (snaps != nullptr && (i % kSnapEvery) == 0 && r < n) {  // s = the state of block i
+        uint64_t* sp = snaps + ((size_t)r * snap_count(cfg) + (size_t)(i / kSnapEvery)) * 25;
+#pragma unroll
+        for (int w = 0; w < 25; ++w) sp[w] = s[w];
+      }
       while (i - (int64_t)min(*vcons, *vstor) >= (int64_t)kDepth) __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
       uint64_t* slot = ring + (i % kDepth) * kSlot;
@@ -195,7 +214,8 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
       }
       // every row below n is stored (also reports rejected before this kernel): k_accum_spec
       // subtracts a rejected row's stored words from the column sums, which include it
-      const bool st_row = spec_lo != nullptr ? r < n : live;
+      // (snapshot mode: nothing is stored, k_fpv_regen rewrites rows when they are needed)
+      const bool st_row = snaps != nullptr ? false : spec_lo != nullptr ? r < n : live;
       if (j0 + 21 <= nd) {  // whole block: 16-B stores (block i starts 16-B aligned iff i even)
         if (st_row) {
           uint8_t* o = om + 8 * j0;
@@ -278,6 +298,49 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
   uint64_t s2[25];
   sponge_one_block(s2, m, cfg.xof);
   squeeze_vec<FO>(s2, cfg.jr_len, out_jr.at(r), cfg.xof, cfg.exact_squeeze);
+}
+
+// The helper's expanded measurement shares of reports [r0, r0 + nr) rewritten into rows 0..nr-1
+// of `out` from k_helper_xof's state snapshots: lane = (report, snapshot), each lane stores its
+// kSnapEvery blocks exactly as the storer wave would have (the share is the raw XOF stream; the
+// fused path checked every element canonical) and permutes between them.
+__global__ void __launch_bounds__(256) k_fpv_regen(Cfg cfg, uint32_t nr, uint32_t r0,
+                                                   const uint64_t* snaps, Rows out) {
+  const uint32_t nsnap = snap_count(cfg);
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (uint64_t)nr * nsnap) return;
+  const uint32_t q = (uint32_t)(gid / nsnap), k = (uint32_t)(gid - (uint64_t)q * nsnap);
+  const int64_t nd = (int64_t)cfg.meas_len * 2, nprod = (nd + 20) / 21;
+  const uint64_t* sp = snaps + ((size_t)(r0 + q) * nsnap + k) * 25;
+  uint64_t s[25];
+#pragma unroll
+  for (int w = 0; w < 25; ++w) s[w] = sp[w];
+  uint8_t* om = out.at(q);
+  const int64_t i0 = (int64_t)k * kSnapEvery;
+  const int64_t i1 = i0 + kSnapEvery < nprod ? i0 + kSnapEvery : nprod;
+  for (int64_t i = i0;; ++i) {
+    const int64_t j0 = 21 * i;
+    if (j0 + 21 <= nd) {  // whole block: 16-B stores (block i starts 16-B aligned iff i even)
+      uint8_t* o = om + 8 * j0;
+      if ((i & 1) == 0) {
+#pragma unroll
+        for (int w = 0; w < 20; w += 2)
+          *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
+        st64(o + 160, s[20]);
+      } else {
+        st64(o, s[0]);
+#pragma unroll
+        for (int w = 1; w < 21; w += 2)
+          *reinterpret_cast<ulonglong2*>(o + 8 * w) = make_ulonglong2(s[w], s[w + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 21; ++w)
+        if (j0 + w < nd) st64(om + 8 * (j0 + w), s[w]);
+    }
+    if (i + 1 >= i1) break;
+    keccak_x(s, cfg.xof);
+  }
 }
 
 // Joint-rand part of an aggregator's own (given) measurement share for few, huge reports

@@ -133,6 +133,14 @@ DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 #ifndef P3G_DIAG_JR_NOABSORB
 #define P3G_DIAG_JR_NOABSORB 0
 #endif
+//   P3G_DIAG_SQ_NOLOAD       the paired Sum query issues no LDS-DMA operand fills (compute only)
+#ifndef P3G_DIAG_SQ_NOLOAD
+#define P3G_DIAG_SQ_NOLOAD 0
+#endif
+//   P3G_DIAG_FW_NOLOAD       k_flp_weights issues no gadget-coefficient fills and no weight flushes
+#ifndef P3G_DIAG_FW_NOLOAD
+#define P3G_DIAG_FW_NOLOAD 0
+#endif
 
 template <>
 struct SqueezeVec<Field128Ops> {
@@ -1011,6 +1019,7 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
       const uint8_t* pr = proof.base + (size_t)row * proof.stride;
       const uint8_t* xr = meas.base + (size_t)row * meas.stride;
       const uint32_t off[4] = {e, e + m, e + h, (uint32_t)min(e + h + m, gp_len - 1u)};
+      if (P3G_DIAG_SQ_NOLOAD) continue;
 #pragma unroll
       for (uint32_t s = 0; s < 4; ++s)
         __builtin_amdgcn_global_load_lds(
@@ -1486,6 +1495,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
       const uint32_t u = (ln & 7u) ^ ((q >> 1) & 7u);
       const uint32_t row = min(r0w + q, n - 1u);
       const uint32_t e = arity + min(kFwChunk * ch + u, gp_len - 1u);
+      if (P3G_DIAG_FW_NOLOAD) continue;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(proof.base + (size_t)row * proof.stride +
                                                           16u * e),
@@ -1502,7 +1512,8 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
     for (uint32_t i = 0; i < 8; ++i) {
       const uint32_t q = 8u * i + ql;
       const T x = FO::load(w + 16u * (8u * q + (u ^ ((q >> 1) & 7u))));
-      if (u < cnt && ((livemask >> q) & 1ull)) FO::store(wm.el(r0w + q, pos + u), x);
+      if (!P3G_DIAG_FW_NOLOAD && u < cnt && ((livemask >> q) & 1ull))
+        FO::store(wm.el(r0w + q, pos + u), x);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };

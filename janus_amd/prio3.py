@@ -314,8 +314,8 @@ class Prio3Gpu:
 
     def set_option(self, name: str, value: int):
         """Engine option of this context (prio3gpu_ctx_set_option: "speculate", "wires_mfma",
-        "wires_cols", "fused_helper", "jr_ring", "spread", "expand_lds", "jr_lds",
-        "exact_squeeze")."""
+        "wires_cols", "fused_helper", "helper_snap", "snap_chunk", "jr_ring", "spread",
+        "expand_lds", "jr_lds", "exact_squeeze")."""
         check(lib().prio3gpu_ctx_set_option(self._ctx, name.encode(), int(value)),
               f"ctx_set_option({name})")
 

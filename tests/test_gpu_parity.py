@@ -452,6 +452,55 @@ def test_fpvec_helper_two_pass_path_bit_exact(name):
     np.testing.assert_array_equal(ho, b.helper_out)
 
 
+@pytest.mark.parametrize("opts", [{}, {"snap_chunk": 1}, {"snap_chunk": 5}, {"helper_snap": 0}],
+                         ids=["snap", "snap_chunk1", "snap_chunk5", "rows"])
+@pytest.mark.parametrize("name", ["fp16_3", "fp64_4", "fp16_300"])
+def test_fpvec_helper_snapshot_mode(name, opts):
+    """Snapshot mode (helper_snap, the default): the FixedPoint helper keeps k_helper_xof's sponge
+    snapshots instead of the expanded share and k_fpv_regen rewrites each query / accumulation
+    chunk's rows.  Prep shares, output shares and the aggregate with a rejected row (regenerated
+    rows summed directly) equal the oracle's, for one chunk, several chunks and the stored-rows
+    mode."""
+    b = batch(name)
+    v = gpu_vdaf(b)
+    for k, val in opts.items():
+        v.set_option(k, val)
+    hs = v.new_state(1, b.n)
+    hp, hst = v.prepare_init(hs, b.nonces, b.public, b.helper_in)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(hp, b.helper_prep)
+    ho, hst2 = v.prepare_next(hs, b.prep_msg, hst.copy())
+    assert (hst2 == 0).all()
+    np.testing.assert_array_equal(ho, b.helper_out)
+    hst = hst.copy()
+    hst[1] = 5
+    hagg = v.new_aggregate(1)
+    v.prepare_next(hs, b.prep_msg, hst, want_output_shares=False, agg=hagg)
+    slots = np.zeros(b.n, np.uint32)
+    slots[1] = 1
+    exp, ecnt = expected_aggregate(b, "helper", slots=slots, slot=0)
+    assert hagg.read(0) == (exp, ecnt) and ecnt == b.n - 1
+
+
+def test_fpvec_helper_snapshot_whole_waves():
+    """64 FixedPoint reports, all accepted, one slot: the snapshot-mode helper aggregates from the
+    storer's column sums alone (every element, no row read or regenerated); the aggregate equals
+    the oracle's and the stored-rows mode's."""
+    b = make_batch("fp16_3", 64)
+    aggs = []
+    for snap in (1, 0):
+        v = gpu_vdaf(b)
+        v.set_option("helper_snap", snap)
+        ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+        lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+        hagg = v.new_aggregate(1)
+        msgs, hst = v.helper_init(hs, b.nonces, b.public, b.helper_in, lp, agg=hagg)
+        assert (hst == 0).all()
+        np.testing.assert_array_equal(msgs, b.prep_msg)
+        aggs.append(hagg.read(0))
+    assert aggs[0] == aggs[1] == expected_aggregate(b, "helper")
+
+
 @pytest.mark.parametrize("opts", [{}, {"jr_ring": 0}, {"spread": 0}],
                          ids=["ring", "k_jr_spread", "k_jr_packed"])
 @pytest.mark.parametrize("name", ["fp16_3", "fp16_300"])
