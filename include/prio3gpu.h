@@ -147,6 +147,8 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
  *                   regenerated rows of one chunk are the only full-size helper scratch)
  *   "jr_ring"       1: FixedPoint leader joint-rand part via k_jr_ring; 0: k_jr
  *   "spread"        1: latency-bound sponge launches take one CU per workgroup
+ *   "spread_lds"    the dynamic LDS bytes that spreading requests (default 98304 = one workgroup
+ *                   per CU; <= 81920 lets two, e.g. a leader's and a helper's, share a CU)
  *   "expand_lds", "jr_lds"  dynamic LDS bytes per k_expand / k_jr block (0 = none): caps those
  *                   kernels' occupancy so another context's kernels fit beside them
  *   "exact_squeeze" test switch: every XOF squeeze takes the exact per-element rejection path

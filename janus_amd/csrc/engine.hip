@@ -201,6 +201,9 @@ struct prio3gpu_ctx {
   bool helper_snap = true;
   uint32_t snap_chunk = 512;  // "snap_chunk": reports per FixedPoint query / regeneration chunk
   bool spread = true;        // "spread": one CU per workgroup for latency-bound sponge launches
+  // "spread_lds": the dynamic LDS such a workgroup requests (96 KB: one per CU; <= 80 KB lets a
+  // leader and a helper workgroup share a CU when both aggregators run on one GPU)
+  size_t spread_lds = 96 * 1024;
   bool jr_ring = true;       // "jr_ring": FixedPoint leader joint-rand part via k_jr_ring
   bool wires_mfma = true;    // "wires_mfma": SumVec chunk > 64 wire pass on the matrix cores
   bool wires_cols = true;    // "wires_cols": chunk <= 64 lane-per-column wire pass
@@ -537,8 +540,7 @@ int copy_out(prio3gpu_ctx* c, void* dst, const void* dev_src, size_t bytes) {
 
 dim3 grid1(size_t n, uint32_t tpb) { return dim3((unsigned)((n + tpb - 1) / tpb)); }
 
-// Dynamic LDS that leaves no room for a second workgroup on the CU (160 KB each).
-constexpr size_t kSpreadLds = 96 * 1024;
+// Spreading: a workgroup requests c->spread_lds of dynamic LDS, so no second one fits its CU.
 bool spread_ok(const prio3gpu_ctx* c, uint32_t blocks) { return c->spread && blocks <= c->cus; }
 
 // Measurement-share words that k_jr absorbs through its LDS window ("fast" blocks 1..lf cover
@@ -736,7 +738,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
           PROF(KID_HELPER_XOF);
           hipLaunchKernelGGL(k_helper_xof<kHxDepth>, dim3((N + kHxRows - 1) / kHxRows),
                              dim3(3 * kHxRows),
-                             spread_ok(c, (N + kHxRows - 1) / kHxRows) ? kSpreadLds : 0,
+                             spread_ok(c, (N + kHxRows - 1) / kHxRows) ? c->spread_lds : 0,
                              c->stream, g, N,
                              CRows{d_in, in_pitch}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
@@ -787,7 +789,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     if (g.jr_len > 0 && g.kind == KIND_FPVEC && c->jr_ring && c->jr_lds == 0 &&
         spread_ok(c, (N + 63) / 64)) {
       PROF(KID_JR_RING);
-      hipLaunchKernelGGL(k_jr_ring, dim3((N + 63) / 64), dim3(2 * kHxRows), kSpreadLds, c->stream,
+      hipLaunchKernelGGL(k_jr_ring, dim3((N + 63) / 64), dim3(2 * kHxRows), c->spread_lds, c->stream,
                          g, N, (uint32_t)st->agg_id, nonces, pub, blinds, meas,
                          Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
                          Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, spec_lo, spec_cy);
@@ -800,7 +802,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
       // a wave per CU when there are few (see spread_ok); otherwise 4-wave blocks
       const bool sp = c->jr_lds == 0 && spread_ok(c, (N + 63) / 64);
       const uint32_t tpb = sp ? 64u : TPB;
-      const size_t jr_lds = sp ? kSpreadLds
+      const size_t jr_lds = sp ? c->spread_lds
                                : std::max<size_t>((TPB / 64) * kJrWaveLds,
                                                   std::min<size_t>(c->jr_lds, 160 * 1024));
       hipLaunchKernelGGL(k_jr<FO>, grid1(n, tpb), dim3(tpb), jr_lds, c->stream, g, N,
@@ -1733,6 +1735,12 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
     c->speculate = on;
   } else if (k == "fused_helper") {
     c->fused_helper = on;
+  } else if (k == "spread_lds") {
+    if (value < 16 * 1024 || value > 160 * 1024) {
+      set_err("option spread_lds: %lld bytes is outside [16384, 163840]", (long long)value);
+      return PRIO3GPU_E_ARG;
+    }
+    c->spread_lds = (size_t)value;
   } else if (k == "helper_snap") {
     c->helper_snap = on;
   } else if (k == "snap_chunk") {
