@@ -145,7 +145,15 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
  *                   (FLP query, accumulation past the column sums, output shares); 0: full rows
  *   "snap_chunk"    reports per FixedPoint query / regeneration chunk (default 512; the
  *                   regenerated rows of one chunk are the only full-size helper scratch)
+ *   "query_overlap" 1: the snapshot-mode helper query regenerates half-chunk i + 1 on a second
+ *                   stream while half-chunk i is queried (two scratch halves); 0 (default): in
+ *                   turn
+ *   "wave_prio"     1: FixedPoint chain waves (k_helper_xof, k_jr_ring) issue at s_setprio 3 and
+ *                   the FixedPoint matrix-core wire passes at 2 over co-running waves; 0: all at 0
  *   "jr_ring"       1: FixedPoint leader joint-rand part via k_jr_ring; 0: k_jr
+ *   "chain_pairs"   64-report chains per k_helper_xof / k_jr_ring workgroup: 1, 2, or 0 (auto,
+ *                   default: 2 once the launch would take more than half the CUs, so a leader's
+ *                   and a helper's launches side by side keep one sponge wave per SIMD)
  *   "spread"        1: latency-bound sponge launches take one CU per workgroup
  *   "spread_lds"    the dynamic LDS bytes that spreading requests (default 98304 = one workgroup
  *                   per CU; <= 81920 lets two, e.g. a leader's and a helper's, share a CU)

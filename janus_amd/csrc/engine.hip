@@ -19,6 +19,7 @@
 #include "prio3_kernels.h"
 #include "fpvec_kernels.h"
 #include "wires_mfma.h"
+#include "fpvec_mfma.h"
 
 using namespace p3g;
 
@@ -187,6 +188,11 @@ struct prio3gpu_ctx {
   uint8_t vk[16];
   int device = 0;
   hipStream_t stream = nullptr;
+  // snapshot-mode helper query: k_fpv_regen of the next half-chunk runs on `aux` beside the
+  // current half-chunk's query on `stream` (created on first use); aux_ev[0..1] regenerated,
+  // aux_ev[2..3] read, per scratch half
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_ev[4] = {};
   DevBuf twiddles, twiddles1, twiddles2;
   // generic staging (inputs given as host pointers) and scratch
   DevBuf io[6];
@@ -205,6 +211,14 @@ struct prio3gpu_ctx {
   // leader and a helper workgroup share a CU when both aggregators run on one GPU)
   size_t spread_lds = 96 * 1024;
   bool jr_ring = true;       // "jr_ring": FixedPoint leader joint-rand part via k_jr_ring
+  // "chain_pairs": 64-report chains per k_helper_xof / k_jr_ring workgroup (0: auto -- 1 while the
+  // launch takes at most half the CUs, else 2, so a leader and a helper launch side by side
+  // still give every sponge wave its own SIMD)
+  uint32_t chain_pairs = 0;
+  // "query_overlap": snapshot-mode helper query regenerates half-chunk i+1 on a second stream
+  // while half-chunk i is queried (two scratch halves; 0, the default: regenerate and query in
+  // turn -- measured faster: the VALU-bound regeneration starves the co-running wire passes)
+  bool query_overlap = false;
   bool wires_mfma = true;    // "wires_mfma": SumVec chunk > 64 wire pass on the matrix cores
   bool wires_cols = true;    // "wires_cols": chunk <= 64 lane-per-column wire pass
   size_t expand_lds = 0;     // "expand_lds": dynamic LDS per k_expand block (occupancy cap)
@@ -237,22 +251,25 @@ struct ProfScope {
   prio3gpu_ctx* c;
   int kid;
   hipEvent_t a{}, b{};
-  ProfScope(prio3gpu_ctx* c_, int kid_) : c(c_), kid(kid_) {
+  hipStream_t s;
+  ProfScope(prio3gpu_ctx* c_, int kid_, hipStream_t s_ = nullptr)
+      : c(c_), kid(kid_), s(s_ ? s_ : c_->stream) {
     if (c->prof.on) {
       a = c->prof.get();
       b = c->prof.get();
-      (void)hipEventRecord(a, c->stream);
+      (void)hipEventRecord(a, s);
     }
   }
   ~ProfScope() {
     if (c->prof.on) {
-      (void)hipEventRecord(b, c->stream);
+      (void)hipEventRecord(b, s);
       c->prof.recs.push_back({kid, a, b});
     }
   }
 };
 }  // namespace
 #define PROF(kid) ProfScope prof_scope_##kid(c, kid)
+#define PROF_ON(kid, strm) ProfScope prof_scope_##kid(c, kid, strm)
 
 struct prio3gpu_state {
   prio3gpu_ctx* ctx = nullptr;
@@ -365,6 +382,7 @@ int upload_tables(DevBuf& buf, uint32_t m, uint32_t calls, uint32_t es) {
 int setup_cfg(prio3gpu_ctx* c, int kind, uint32_t bits, uint32_t length, uint32_t chunk) {
   Cfg& g = c->cfg;
   g.kind = (uint32_t)kind;
+  g.wave_prio = 1u;
   // VDAF-07 algorithm IDs: Count 0, Sum 1, SumVec 2, Histogram 3; FixedPoint L2 0xFFFF0000
   g.algo_id = kind == PRIO3GPU_FPVEC ? 0xFFFF0000u : (uint32_t)kind;
   g.qr_len = kind == PRIO3GPU_FPVEC ? 2u : 1u;
@@ -543,6 +561,12 @@ dim3 grid1(size_t n, uint32_t tpb) { return dim3((unsigned)((n + tpb - 1) / tpb)
 // Spreading: a workgroup requests c->spread_lds of dynamic LDS, so no second one fits its CU.
 bool spread_ok(const prio3gpu_ctx* c, uint32_t blocks) { return c->spread && blocks <= c->cus; }
 
+// 64-report chains per FixedPoint chain workgroup (option chain_pairs).
+uint32_t chain_pairs(const prio3gpu_ctx* c, size_t n) {
+  if (c->chain_pairs) return c->chain_pairs;
+  return (n + 63) / 64 > std::max<uint32_t>(1u, c->cus / 2) ? 2u : 1u;
+}
+
 // Measurement-share words that k_jr absorbs through its LDS window ("fast" blocks 1..lf cover
 // words [16, 21 (lf+1) - 5)); elements [e0, e1) lie entirely inside.  Field128 types with JR only.
 bool spec_range(const Cfg& g, uint32_t& nd, uint32_t& e0, uint32_t& e1) {
@@ -561,17 +585,31 @@ bool spec_range(const Cfg& g, uint32_t& nd, uint32_t& e0, uint32_t& e1) {
 }
 
 // Snapshot mode: the helper's expanded measurement shares of reports [r0, r0 + nr) rewritten
-// from k_helper_xof's sponge snapshots into st->scratch rows 0..nr-1 (k_fpv_regen).
-int regen_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t nr) {
+// from k_helper_xof's sponge snapshots into rows 0..nr-1 of `dst` (default st->scratch, which is
+// then sized for them), on `strm` (default the context's stream) (k_fpv_regen).
+int regen_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t nr, uint8_t* dst = nullptr,
+               hipStream_t strm = nullptr) {
   const Cfg& g = c->cfg;
   const size_t row = (size_t)g.meas_len * g.es;
-  CHK(st->scratch.ensure(nr * row));
+  if (!dst) {
+    CHK(st->scratch.ensure(nr * row));
+    dst = st->scratch.u8();
+  }
+  if (!strm) strm = c->stream;
   const uint64_t lanes = (uint64_t)nr * snap_count(g);
-  PROF(KID_FPV_REGEN);
-  hipLaunchKernelGGL(k_fpv_regen, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, c->stream, g,
+  PROF_ON(KID_FPV_REGEN, strm);
+  hipLaunchKernelGGL(k_fpv_regen, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, strm, g,
                      (uint32_t)nr, (uint32_t)r0, reinterpret_cast<const uint64_t*>(st->snaps.p),
-                     Rows{st->scratch.u8(), row});
+                     Rows{dst, row});
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// The context's auxiliary stream and its four events (created on first use).
+int ensure_aux(prio3gpu_ctx* c) {
+  if (!c->aux) HIPCHK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+  for (auto& e : c->aux_ev)
+    if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return 0;
 }
 
@@ -580,10 +618,30 @@ size_t fpv_chunk(const prio3gpu_ctx* c, const prio3gpu_state* st, size_t n) {
   return std::max<size_t>(1, std::min<size_t>({n, (size_t)c->snap_chunk, st->fpart_rows}));
 }
 
-// FixedPointBoundedL2VecSum FLP query (fpvec_kernels.h): weights, wire passes, finalize, over
-// reports [r0, r0 + n) (rows 0..n-1 of `meas` and `proof`; the state's per-report arrays at r0).
+// FixedPointBoundedL2VecSum FLP query (fpvec_kernels.h), first part: the report flags and
+// k_fpv_weights (Lagrange weights, p(t), gadget-output sums: the proof share and the randomness
+// only, no measurement row) for the whole batch, so the chunked wire passes do not wait for it.
+int launch_fpv_weights(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows proof,
+                       uint8_t* d_status) {
+  const Cfg& g = c->cfg;
+  const FpvW W = fpv_w_layout(g);
+  Rows wrows{st->w.u8(), (size_t)W.len * 16};
+  Rows prep{st->prep.u8(), g.prep_share_len};
+  uint32_t* flags = reinterpret_cast<uint32_t*>(st->flags.p);
+  HIPCHK(hipMemsetAsync(flags, 0, n * 4, c->stream));
+  const size_t lds = (size_t)16 * (3 * (size_t)g.m + g.chunk + 1 + 12) + 16;
+  PROF(KID_FPV_WEIGHTS);
+  hipLaunchKernelGGL(k_fpv_weights, dim3((uint32_t)n, 2), dim3(256), lds, c->stream, g,
+                     (uint32_t)n, proof, CRows{st->t.u8(), 32}, CRows{st->jr.u8(), 32}, prep,
+                     d_status, wrows, flags);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// Second part: wire passes and finalize over reports [r0, r0 + n) (rows 0..n-1 of `meas`; the
+// state's per-report arrays at r0; d_status at r0).
 int launch_fpv_query_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t n, CRows meas,
-                          CRows proof, uint8_t* d_status) {
+                          uint8_t* d_status) {
   const Cfg& g = c->cfg;
   const uint32_t N = (uint32_t)n;
   const uint32_t H = fpv_rows(g);
@@ -591,30 +649,37 @@ int launch_fpv_query_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t
   Rows wrows{st->w.u8() + r0 * (size_t)W.len * 16, (size_t)W.len * 16};
   Rows prep{st->prep.u8() + r0 * g.prep_share_len, g.prep_share_len};
   uint32_t* flags = reinterpret_cast<uint32_t*>(st->flags.p) + r0;
-  const CRows tq{st->t.u8() + r0 * 32, 32}, jr{st->jr.u8() + r0 * 32, 32};
+  const CRows jr{st->jr.u8() + r0 * 32, 32};
   const CRows part{st->part.u8() + r0 * 16, 16};
-  HIPCHK(hipMemsetAsync(flags, 0, n * 4, c->stream));
-  const size_t lds = (size_t)16 * (3 * (size_t)g.m + g.chunk + 1 + 12) + 16;
-  {
-    PROF(KID_FPV_WEIGHTS);
-    hipLaunchKernelGGL(k_fpv_weights, dim3(N, 2), dim3(256), lds, c->stream, g, N, proof, tq, jr,
-                       prep, d_status, wrows, flags);
-  }
+  // matrix-core wire passes (fpvec_mfma.h) unless the option is off or the digit windows of a
+  // call range would not fit 64 KB of LDS; gadget 1 on them for 16- and 32-bit entries
+  const bool m0 = c->wires_mfma && fpv_w0m_lds(g) <= 64 * 1024 && H >= kFpvMfmaH;
+  const bool m1 = c->wires_mfma && fpv_w1m_bits_ok(g.bits) && fpv_w1m_lds(g) <= 64 * 1024;
+  const uint32_t H0 = m0 ? kFpvMfmaH : H;  // partial row groups k_fpv_finalize folds
   {
     PROF(KID_FPV_WIRES0);
-    hipLaunchKernelGGL(k_fpv_wires0, dim3((g.chunk + 255) / 256, H, N), dim3(256), 0, c->stream, g,
-                       N, H, meas, CRows{wrows.base, wrows.stride}, d_status, st->fpart.u8(),
-                       flags);
+    if (m0)
+      hipLaunchKernelGGL(k_fpv_wires0_mfma, dim3(kFpvMfmaH, N), dim3(256), fpv_w0m_lds(g),
+                         c->stream, g, N, meas, CRows{wrows.base, wrows.stride}, d_status,
+                         st->fpart.u8(), flags);
+    else
+      hipLaunchKernelGGL(k_fpv_wires0, dim3((g.chunk + 255) / 256, H, N), dim3(256), 0, c->stream,
+                         g, N, H, meas, CRows{wrows.base, wrows.stride}, d_status, st->fpart.u8(),
+                         flags);
   }
   {
     PROF(KID_FPV_WIRES1);
-    hipLaunchKernelGGL(k_fpv_wires1, dim3((g.chunk1 + 255) / 256, N), dim3(256), 0, c->stream, g, N,
-                       meas, CRows{wrows.base, wrows.stride}, prep, d_status);
+    if (m1)
+      hipLaunchKernelGGL(k_fpv_wires1_mfma, dim3(N), dim3(256), fpv_w1m_lds(g), c->stream, g, N,
+                         meas, CRows{wrows.base, wrows.stride}, prep, d_status);
+    else
+      hipLaunchKernelGGL(k_fpv_wires1, dim3((g.chunk1 + 255) / 256, N), dim3(256), 0, c->stream, g,
+                         N, meas, CRows{wrows.base, wrows.stride}, prep, d_status);
   }
   {
     PROF(KID_FPV_FINAL);
     hipLaunchKernelGGL(k_fpv_finalize, dim3((g.chunk + 255) / 256, N), dim3(256), 0, c->stream, g,
-                       N, H, meas, CRows{wrows.base, wrows.stride}, jr, part, st->fpart.u8(), prep,
+                       N, H0, meas, CRows{wrows.base, wrows.stride}, jr, part, st->fpart.u8(), prep,
                        d_status, flags);
   }
   HIPCHK(hipGetLastError());
@@ -627,6 +692,28 @@ int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, 
                      uint8_t* d_status) {
   const Cfg& g = c->cfg;
   const size_t ch = fpv_chunk(c, st, n);
+  CHK(launch_fpv_weights(c, st, n, proof, d_status));
+  if (st->snap_active && c->query_overlap && n > 1) {
+    // Half-chunks through two scratch halves: k_fpv_regen of half-chunk i + 1 (aux stream, a
+    // VALU-bound sponge pass) runs beside the query of half-chunk i (HBM-bound wire passes).
+    // regen(i) waits for query(i - 2), which read the same half; query(i) waits for regen(i).
+    const size_t hc = std::max<size_t>(1, (ch + 1) / 2), row = (size_t)g.meas_len * g.es;
+    CHK(st->scratch.ensure(2 * hc * row));
+    CHK(ensure_aux(c));
+    HIPCHK(hipEventRecord(c->aux_ev[2], c->stream));  // the snapshots are written
+    HIPCHK(hipStreamWaitEvent(c->aux, c->aux_ev[2], 0));
+    for (size_t i = 0, r0 = 0; r0 < n; ++i, r0 += hc) {
+      const size_t nr = std::min(hc, n - r0), h = i & 1;
+      uint8_t* buf = st->scratch.u8() + h * hc * row;
+      if (i >= 2) HIPCHK(hipStreamWaitEvent(c->aux, c->aux_ev[2 + h], 0));
+      CHK(regen_rows(c, st, r0, nr, buf, c->aux));
+      HIPCHK(hipEventRecord(c->aux_ev[h], c->aux));
+      HIPCHK(hipStreamWaitEvent(c->stream, c->aux_ev[h], 0));
+      CHK(launch_fpv_query_rows(c, st, r0, nr, CRows{buf, row}, d_status + r0));
+      HIPCHK(hipEventRecord(c->aux_ev[2 + h], c->stream));
+    }
+    return 0;
+  }
   for (size_t r0 = 0; r0 < n; r0 += ch) {
     const size_t nr = std::min(ch, n - r0);
     CRows m{meas.base + r0 * meas.stride, meas.stride};
@@ -634,8 +721,7 @@ int launch_fpv_query(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, CRows meas, 
       CHK(regen_rows(c, st, r0, nr));
       m = CRows{st->scratch.u8(), (size_t)g.meas_len * g.es};
     }
-    CHK(launch_fpv_query_rows(c, st, r0, nr, m, CRows{proof.base + r0 * proof.stride, proof.stride},
-                              d_status + r0));
+    CHK(launch_fpv_query_rows(c, st, r0, nr, m, d_status + r0));
   }
   return 0;
 }
@@ -736,10 +822,12 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
         HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
         {
           PROF(KID_HELPER_XOF);
-          hipLaunchKernelGGL(k_helper_xof<kHxDepth>, dim3((N + kHxRows - 1) / kHxRows),
-                             dim3(3 * kHxRows),
-                             spread_ok(c, (N + kHxRows - 1) / kHxRows) ? c->spread_lds : 0,
-                             c->stream, g, N,
+          const uint32_t P = chain_pairs(c, n), rows = P * kHxRows;
+          const uint32_t blocks = (N + rows - 1) / rows;
+          const size_t lds = std::max<size_t>(P * kHxRingBytes,
+                                              spread_ok(c, blocks) ? c->spread_lds : 0);
+          auto kern = P == 2 ? k_helper_xof<kHxDepth, 2> : k_helper_xof<kHxDepth, 1>;
+          hipLaunchKernelGGL(kern, dim3(blocks), dim3(3 * rows), lds, c->stream, g, N,
                              CRows{d_in, in_pitch}, nonces, pub, mo, po,
                              Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
                              Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb,
@@ -786,10 +874,14 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
   bool ring_done = false;
   if constexpr (FO::ES == 16) {
     // few huge FixedPoint reports: sponge wave + loader wave per CU (k_jr_ring)
+    const uint32_t P = chain_pairs(c, n), rows = P * kHxRows;
+    const uint32_t blocks = (N + rows - 1) / rows;
     if (g.jr_len > 0 && g.kind == KIND_FPVEC && c->jr_ring && c->jr_lds == 0 &&
-        spread_ok(c, (N + 63) / 64)) {
+        spread_ok(c, blocks)) {
       PROF(KID_JR_RING);
-      hipLaunchKernelGGL(k_jr_ring, dim3((N + 63) / 64), dim3(2 * kHxRows), c->spread_lds, c->stream,
+      const size_t lds = std::max<size_t>(P * kHxRingBytes, c->spread_lds);
+      auto kern = P == 2 ? k_jr_ring<2> : k_jr_ring<1>;
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(2 * rows), lds, c->stream,
                          g, N, (uint32_t)st->agg_id, nonces, pub, blinds, meas,
                          Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
                          Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, spec_lo, spec_cy);
@@ -1347,6 +1439,10 @@ int prio3gpu_ctx_destroy(prio3gpu_ctx* c) {
   for (auto ev : c->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
+  if (c->aux) (void)hipStreamSynchronize(c->aux);
+  for (auto ev : c->aux_ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -1753,6 +1849,14 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
     c->spread = on;
   } else if (k == "jr_ring") {
     c->jr_ring = on;
+  } else if (k == "query_overlap") {
+    c->query_overlap = on;
+  } else if (k == "chain_pairs") {
+    if (value < 0 || value > 2) {
+      set_err("option chain_pairs: %lld is not 0 (auto), 1 or 2", (long long)value);
+      return PRIO3GPU_E_ARG;
+    }
+    c->chain_pairs = (uint32_t)value;
   } else if (k == "wires_mfma") {
     c->wires_mfma = on;
   } else if (k == "wires_cols") {
@@ -1764,6 +1868,8 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
       return PRIO3GPU_E_ARG;
     }
     (k == "expand_lds" ? c->expand_lds : c->jr_lds) = (size_t)value;
+  } else if (k == "wave_prio") {
+    c->cfg.wave_prio = on ? 1u : 0u;
   } else if (k == "exact_squeeze") {
     // every XOF squeeze takes the exact per-element rejection path (test switch); the FixedPoint
     // helper then runs its exact two-pass XOF

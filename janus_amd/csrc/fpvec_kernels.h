@@ -75,8 +75,10 @@ DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[1
   }
 }
 
-constexpr uint32_t kHxRows = 64;              // reports per workgroup (1 producer + 1 consumer wave)
+constexpr uint32_t kHxRows = 64;              // reports per producer/consumer pair (a wave each)
 constexpr uint32_t kHxDepth = 4;              // ring slots: the producer may run 4 blocks ahead
+// LDS ring bytes of one pair (slot rows kHxRows + 1 words apart; see k_helper_xof)
+constexpr size_t kHxRingBytes = (size_t)kHxDepth * 21 * (kHxRows + 1) * 8;
 
 // Snapshot mode (engine option helper_snap, the default for FixedPoint vectors): instead of
 // storing the 25.6 MB expanded measurement share of every report (entries = 100k), the producer
@@ -91,8 +93,13 @@ __host__ __device__ inline uint32_t snap_count(const Cfg& g) {
 }
 constexpr size_t kSnapBytes = 25 * 8;  // one Keccak state
 
-template <uint32_t kDepth>
-__global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
+// kPairs producer/consumer/storer triples per workgroup (waves p, kPairs + p, 2 kPairs + p for
+// pair p), each with its own ring: the waves of ONE workgroup sit on distinct SIMDs, while two
+// workgroups sharing a CU put their first waves on the same SIMD, so when there are more pairs
+// than CUs (or the other aggregator's chains share the GPU) two pairs per workgroup keep one
+// sponge wave per SIMD.  The ring lives in dynamic LDS (kPairs * kHxRingBytes at launch).
+template <uint32_t kDepth, uint32_t kPairs>
+__global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, uint32_t n, CRows helper_shares,
                                                     CRows nonces, CRows public_shares,
                                                     Rows out_meas, Rows out_proof, Rows out_part,
                                                     Rows out_seed, Rows out_jr,
@@ -103,27 +110,27 @@ __global__ void __launch_bounds__(3 * kHxRows) k_helper_xof(Cfg cfg, uint32_t n,
   // slot rows are kHxRows + 1 words apart: the storer's column reads (words x rows) hit distinct
   // banks; the producer's and consumer's row accesses stay conflict-free
   constexpr uint32_t kStride = kHxRows + 1, kSlot = 21 * kStride;
-  __shared__ uint64_t ring[kDepth * kSlot];
-  // Ring handoff through two LDS counters instead of a per-block s_barrier: the producer
-  // publishes `produced` after its slot writes have landed (lgkmcnt(0)); the consumer publishes
-  // `consumed` after its slot reads have returned.  Neither wave waits for the other's
+  static_assert(kDepth == kHxDepth, "kHxRingBytes assumes kHxDepth slots");
+  extern __shared__ __attribute__((aligned(16))) uint64_t hx_dyn[];
+  // Ring handoff through LDS counters instead of a per-block s_barrier: the producer publishes
+  // `produced` after its slot writes have landed (lgkmcnt(0)); the consumer publishes `consumed`
+  // (the storer `stored`) after its slot reads have returned.  Neither wave waits for the other's
   // permutation unless the ring is full / empty, so each runs at its own pace.
-  __shared__ uint32_t produced, consumed, stored;
-  volatile uint32_t* vprod = &produced;
-  volatile uint32_t* vcons = &consumed;
-  volatile uint32_t* vstor = &stored;
-  if (threadIdx.x == 0) {
-    produced = 0u;
-    consumed = 0u;
-    stored = 0u;
-  }
-  __syncthreads();
-  // wave 0 produces, wave 1 consumes, wave 2 stores the expanded share to HBM (measured: 2
-  // producer + 2 consumer waves per workgroup ran 9 % slower)
+  __shared__ uint32_t counters[3 * kPairs];
   const uint32_t lane = threadIdx.x & (kHxRows - 1u);
   const uint32_t wave = threadIdx.x / kHxRows;  // wave-uniform roles
-  const bool producer = wave == 0u, storer = wave == 2u;
-  const uint32_t r0 = blockIdx.x * kHxRows;
+  const uint32_t pair = wave % kPairs, role = wave / kPairs;
+  uint64_t* ring = hx_dyn + (size_t)pair * (kDepth * kSlot);
+  volatile uint32_t* vprod = &counters[3 * pair];
+  volatile uint32_t* vcons = &counters[3 * pair + 1];
+  volatile uint32_t* vstor = &counters[3 * pair + 2];
+  if (threadIdx.x < 3 * kPairs) counters[threadIdx.x] = 0u;
+  __syncthreads();
+  // role 0 produces, role 1 consumes, role 2 stores the expanded share to HBM / sums its columns
+  const bool producer = role == 0u, storer = role == 2u;
+  const uint32_t r0 = (blockIdx.x * kPairs + pair) * kHxRows;
+  if (r0 >= n) return;  // a whole pair past the batch (no barrier follows)
+  if (cfg.wave_prio) __builtin_amdgcn_s_setprio(3);  // the chain first on its SIMD
   const uint32_t r = r0 + lane;
   const bool live = r < n && (!status || status[r] == ST_OK);
   const uint32_t rr = r < n ? r : n - 1u;  // every lane runs the loop, clamped row
@@ -350,9 +357,12 @@ __global__ void __launch_bounds__(256) k_fpv_regen(Cfg cfg, uint32_t nr, uint32_
 // speculative column sums k_accum_spec consumes (every share word, same layout and row clamp as
 // k_jr), while the sponge wave only absorbs and permutes.  Ring rows are 65 words apart so the
 // loader's column reads (lane = word) hit distinct banks.
+// kPairs sponge/loader pairs per workgroup (waves p and kPairs + p), rings in dynamic LDS
+// (kPairs * kHxRingBytes at launch), for the reason k_helper_xof gives.
 constexpr uint32_t kJrRingStride = kHxRows + 1;
 
-__global__ void __launch_bounds__(2 * kHxRows) k_jr_ring(Cfg cfg, uint32_t n, uint32_t agg_id,
+template <uint32_t kPairs>
+__global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint32_t n, uint32_t agg_id,
                                                  CRows nonces, CRows public_shares,
                                                  CRows blinds, CRows meas, Rows out_part,
                                                  Rows out_seed, Rows out_jr,
@@ -360,18 +370,20 @@ __global__ void __launch_bounds__(2 * kHxRows) k_jr_ring(Cfg cfg, uint32_t n, ui
                                                  uint8_t* spec_cy) {
   using FO = Field128Ops;
   constexpr uint32_t kSlot = 21 * kJrRingStride;
-  __shared__ uint64_t ring[kHxDepth * kSlot];
-  __shared__ uint32_t produced, consumed;
-  volatile uint32_t* vprod = &produced;
-  volatile uint32_t* vcons = &consumed;
-  if (threadIdx.x == 0) {
-    produced = 0u;
-    consumed = 0u;
-  }
-  __syncthreads();
+  extern __shared__ __attribute__((aligned(16))) uint64_t jr_dyn[];
+  __shared__ uint32_t counters[2 * kPairs];
   const uint32_t lane = threadIdx.x & (kHxRows - 1u);
-  const bool loader = threadIdx.x >= kHxRows;  // wave 0: sponge, wave 1: loader
-  const uint32_t r0 = blockIdx.x * kHxRows;
+  const uint32_t wave = threadIdx.x / kHxRows;
+  const uint32_t pair = wave % kPairs;
+  const bool loader = wave >= kPairs;  // waves 0..kPairs-1: sponges, then the loaders
+  uint64_t* ring = jr_dyn + (size_t)pair * (kHxDepth * kSlot);
+  volatile uint32_t* vprod = &counters[2 * pair];
+  volatile uint32_t* vcons = &counters[2 * pair + 1];
+  if (threadIdx.x < 2 * kPairs) counters[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint32_t r0 = (blockIdx.x * kPairs + pair) * kHxRows;
+  if (r0 >= n) return;  // a whole pair past the batch (no barrier follows)
+  if (cfg.wave_prio) __builtin_amdgcn_s_setprio(3);  // the chain first on its SIMD
   const uint32_t r = r0 + lane;
   const bool live = r < n && (!status || status[r] == ST_OK);
   const uint32_t rr = r < n ? r : n - 1u;  // rows past n: the last row (k_jr's clamp)

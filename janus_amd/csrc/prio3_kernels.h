@@ -59,6 +59,9 @@ struct Cfg {
   uint32_t leader_share_len, helper_share_len, public_share_len, prep_share_len, prep_msg_len;
   uint32_t qr_len;          // query-randomness elements (one per gadget)
   uint32_t exact_squeeze;   // test switch: every XOF squeeze takes the per-element path
+  // engine option wave_prio: FixedPoint chain waves issue at s_setprio 3 and its matrix-core wire
+  // passes at 2, over whatever co-runs on their SIMDs (the other aggregator's query, k_fpv_regen)
+  uint32_t wave_prio;
   Xof xof;                  // XofShake128 (default) or XofTurboShake128
   const uint8_t* twiddles;  // device: alpha_m^k, k < m, Montgomery form, ES bytes each
   // FixedPointBoundedL2VecSum's second gadget, ParallelSum(PolyEval(norm poly), chunk1)

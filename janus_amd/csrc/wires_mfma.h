@@ -58,6 +58,65 @@ DEVI uint64_t shfl_xor_u64(uint64_t v, int m) {
 }
 
 
+// One column's wire from its exact MFMA sum: T[w] = signed 32-bit word w (rows 4w .. 4w + 3 of
+// the C/D fragment) of sum_k w_k x'_k.  Adds K128 * W' with W' = (sum_k w_k mod p) + calls p
+// (>= the integer sum of the weights, so the total is >= 0 and == sum_k w_k x_k mod p; `wsum` is
+// the weights' sum mod p) and REDCs it like the VALU path.
+DEVI F128 wires_mfma_finish(const int64_t T[8], const F128& wsum, uint32_t calls) {
+  uint32_t S[10];
+  {
+    int64_t cr = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const int64_t v = T[w] + cr;
+      S[w] = (uint32_t)v;
+      cr = v >> 32;
+    }
+    S[8] = (uint32_t)cr;
+    S[9] = (uint32_t)(cr >> 32);
+  }
+  uint32_t Wd[6];
+  {
+    const int64_t CC = (int64_t)calls;
+    const int64_t v[5] = {(int64_t)wsum.w[0] + CC, (int64_t)wsum.w[1],
+                          (int64_t)wsum.w[2] - 28 * CC, (int64_t)wsum.w[3], CC};
+    int64_t cr = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int64_t t = v[q] + cr;
+      Wd[q] = (uint32_t)t;
+      cr = t >> 32;
+    }
+    Wd[5] = (uint32_t)cr;
+  }
+  uint32_t M[7];
+  uint64_t mc = 0;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const uint64_t v = (uint64_t)Wd[q] * 0x80808080u + mc;
+    M[q] = (uint32_t)v;
+    mc = v >> 32;
+  }
+  M[6] = (uint32_t)mc;
+  uint64_t sc = 0;
+#pragma unroll
+  for (int w = 0; w < 10; ++w) {
+    uint64_t v = (uint64_t)S[w] + sc;
+#pragma unroll
+    for (int sft = 0; sft < 4; ++sft)
+      if (w - sft >= 0 && w - sft < 7) v += M[w - sft];
+    S[w] = (uint32_t)v;
+    sc = v >> 32;
+  }
+  Wide wd;
+  wide_zero(wd);
+#pragma unroll
+  for (int w = 0; w < 6; ++w) wd.lo[w] = S[w];
+  wd.lo[6] = ((uint64_t)S[7] << 32) | S[6];
+  wd.hi[6] = S[8];
+  return wide_reduce(wd);
+}
+
 // Block per report, a wave per 32-column tile (<= 4 waves, then tiles loop).  (A wave-per-report
 // form for short rows, chunk 8..32, measured slower than k_flp_wires_cols -- 3.9 vs 1.66 ms per
 // launch on Histogram256, profiles/r03/ab_wires_mfma_short_r3u.log -- and was removed.)
@@ -197,63 +256,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       T[2 * g] = h ? rv : gown[g];
       T[2 * g + 1] = h ? gown[g] : rv;
     }
-    uint32_t S[10];
-    {
-      int64_t cr = 0;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) {
-        const int64_t v = T[w] + cr;
-        S[w] = (uint32_t)v;
-        cr = v >> 32;
-      }
-      S[8] = (uint32_t)cr;
-      S[9] = (uint32_t)(cr >> 32);
-    }
-    // + K128 * W', W' = (sum_k w_k mod p) + calls p >= sum_k w_k (the integer), so the total stays
-    // >= 0 and == sum_k w_k x_k (mod p); the sums come from k_flp_weights (SMM, SLM)
-    {
-      const F128 wsum = FO::load(wm.el(r, h ? W.slm() : W.smm()));
-      uint32_t Wd[6];
-      {
-        const int64_t CC = (int64_t)C;
-        const int64_t v[5] = {(int64_t)wsum.w[0] + CC, (int64_t)wsum.w[1],
-                              (int64_t)wsum.w[2] - 28 * CC, (int64_t)wsum.w[3], CC};
-        int64_t cr = 0;
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-          const int64_t t = v[q] + cr;
-          Wd[q] = (uint32_t)t;
-          cr = t >> 32;
-        }
-        Wd[5] = (uint32_t)cr;
-      }
-      uint32_t M[7];
-      uint64_t mc = 0;
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const uint64_t v = (uint64_t)Wd[q] * 0x80808080u + mc;
-        M[q] = (uint32_t)v;
-        mc = v >> 32;
-      }
-      M[6] = (uint32_t)mc;
-      uint64_t sc = 0;
-#pragma unroll
-      for (int w = 0; w < 10; ++w) {
-        uint64_t v = (uint64_t)S[w] + sc;
-#pragma unroll
-        for (int sft = 0; sft < 4; ++sft)
-          if (w - sft >= 0 && w - sft < 7) v += M[w - sft];
-        S[w] = (uint32_t)v;
-        sc = v >> 32;
-      }
-    }
-    Wide wd;
-    wide_zero(wd);
-#pragma unroll
-    for (int w = 0; w < 6; ++w) wd.lo[w] = S[w];
-    wd.lo[6] = ((uint64_t)S[7] << 32) | S[6];
-    wd.hi[6] = S[8];
-    const F128 v = wide_reduce(wd);
+    const F128 v = wires_mfma_finish(T, FO::load(wm.el(r, h ? W.slm() : W.smm())), C);
     if (colok) {
       // wire 2j + h = L0 s_(2j+h) (- HL for h = 1) + (RP[j] a_j | b_j)
       uint8_t* outp = out_prep.at(r);

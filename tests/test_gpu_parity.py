@@ -452,15 +452,19 @@ def test_fpvec_helper_two_pass_path_bit_exact(name):
     np.testing.assert_array_equal(ho, b.helper_out)
 
 
-@pytest.mark.parametrize("opts", [{}, {"snap_chunk": 1}, {"snap_chunk": 5}, {"helper_snap": 0}],
-                         ids=["snap", "snap_chunk1", "snap_chunk5", "rows"])
+@pytest.mark.parametrize("opts", [{}, {"snap_chunk": 1}, {"snap_chunk": 5}, {"helper_snap": 0},
+                                  {"chain_pairs": 2}, {"snap_chunk": 5, "query_overlap": 1},
+                                  {"snap_chunk": 1, "query_overlap": 1}],
+                         ids=["snap", "snap_chunk1", "snap_chunk5", "rows", "pairs2", "overlap5",
+                              "overlap1"])
 @pytest.mark.parametrize("name", ["fp16_3", "fp64_4", "fp16_300"])
 def test_fpvec_helper_snapshot_mode(name, opts):
     """Snapshot mode (helper_snap, the default): the FixedPoint helper keeps k_helper_xof's sponge
     snapshots instead of the expanded share and k_fpv_regen rewrites each query / accumulation
-    chunk's rows.  Prep shares, output shares and the aggregate with a rejected row (regenerated
-    rows summed directly) equal the oracle's, for one chunk, several chunks and the stored-rows
-    mode."""
+    chunk's rows (in turn, or with query_overlap 1 the query's half-chunks regenerated on a
+    second stream beside the previous half-chunk's query).  Prep shares, output shares and the
+    aggregate with a rejected row (regenerated rows summed directly) equal the oracle's, for one
+    chunk, several chunks and the stored-rows mode."""
     b = batch(name)
     v = gpu_vdaf(b)
     for k, val in opts.items():
@@ -501,8 +505,30 @@ def test_fpvec_helper_snapshot_whole_waves():
     assert aggs[0] == aggs[1] == expected_aggregate(b, "helper")
 
 
-@pytest.mark.parametrize("opts", [{}, {"jr_ring": 0}, {"spread": 0}],
-                         ids=["ring", "k_jr_spread", "k_jr_packed"])
+@pytest.mark.parametrize("pairs", [1, 2])
+def test_fpvec_chain_pairs(pairs):
+    """k_helper_xof / k_jr_ring with one or two 64-report chains per workgroup (option
+    chain_pairs): 100 reports, so the second workgroup's pair is partial and, with two pairs, the
+    first workgroup's second pair too.  Both aggregators' prep shares, the prep messages and both
+    aggregates (the chains' column sums) equal the oracle's."""
+    b = make_batch("fp16_3", 100)
+    v = gpu_vdaf(b)
+    v.set_option("chain_pairs", pairs)
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    assert (lst == 0).all()
+    np.testing.assert_array_equal(lp, b.leader_prep)
+    lagg, hagg = v.new_aggregate(1), v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, b.nonces, b.public, b.helper_in, lp, agg=hagg)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(msgs, b.prep_msg)
+    v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
+    assert lagg.read(0) == expected_aggregate(b, "leader")
+    assert hagg.read(0) == expected_aggregate(b, "helper")
+
+
+@pytest.mark.parametrize("opts", [{}, {"jr_ring": 0}, {"spread": 0}, {"chain_pairs": 2}],
+                         ids=["ring", "k_jr_spread", "k_jr_packed", "ring_pairs2"])
 @pytest.mark.parametrize("name", ["fp16_3", "fp16_300"])
 def test_fpvec_leader_jr_variants(name, opts):
     """The leader's FixedPoint joint-rand part runs k_jr_ring (sponge wave + loader wave writing

@@ -99,3 +99,49 @@ def test_mfma_wires_helper_path(monkeypatch):
         a, cnt = agg.read(0)
         out.append((bytes(a), cnt))
     assert out[0] == out[1]
+
+
+# (bits, entries): FixedPoint16 / 32 take both matrix-core passes (k_fpv_wires0_mfma over 4 call
+# ranges, k_fpv_wires1_mfma over the raw bits); FixedPoint64 takes k_fpv_wires0_mfma and the VALU
+# k_fpv_wires1
+FP_SHAPES = [(16, 300), (16, 5000), (16, 37), (32, 50), (64, 20)]
+
+
+@pytest.mark.parametrize("shape", FP_SHAPES, ids=lambda s: "fp%d_%d" % s)
+def test_fpvec_mfma_wires_match_valu(shape):
+    """FixedPoint wire passes on the matrix cores (fpvec_mfma.h) against the VALU k_fpv_wires0 /
+    k_fpv_wires1 (wires_mfma = 0): random canonical leader shares (all-zero, all-0x7F.. and p - 1
+    rows among them) and non-canonical elements in several position classes; identical prep
+    shares and the same reports rejected."""
+    from janus_amd.prio3 import Prio3Gpu
+    bits, entries = shape
+    vk = bytes(range(16))
+    vm = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(bits, entries, vk)
+    vv = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(bits, entries, vk)
+    vv.set_option("wires_mfma", 0)
+    s = vm.sizes
+    rng = np.random.default_rng(bits * 100003 + entries)
+    n = 96
+    nel = (s.leader_input_share - 16) // 16  # measurement + proof elements, then the blind
+    meas_len = bits * entries + 2 * bits - 2
+    nonces = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    pub = rng.integers(0, 256, size=(n, s.public_share), dtype=np.uint8)
+    lin = rng.integers(0, 256, size=(n, s.leader_input_share), dtype=np.uint8)
+    el = lin[:, :nel * 16].reshape(n, nel, 16)
+    el[:, :, 15] &= 0x7F
+    el[0, :meas_len, :] = 0
+    el[1, :meas_len, :] = 0xFF
+    el[1, :meas_len, 15] = 0x7F
+    el[2, :meas_len, :] = np.frombuffer((2**128 - 28 * 2**64).to_bytes(16, "little"), np.uint8)
+    bad = {5: 0, 9: meas_len - 1, 17: 31, 33: meas_len // 2, 41: bits * entries}
+    for r, e in bad.items():
+        lin[r, e * 16:(e + 1) * 16] = 0xFF
+    # canonical elements the pre-filter flags (top word 2^32 - 1, value < p)
+    lin[50, 16 * 7:16 * 8] = np.frombuffer((2**128 - 29 * 2**64).to_bytes(16, "little"), np.uint8)
+    lpm, stm = vm.prepare_init(vm.new_state(0, n), nonces, pub, lin)
+    lpv, stv = vv.prepare_init(vv.new_state(0, n), nonces, pub, lin)
+    np.testing.assert_array_equal(stm, stv)
+    for r in range(n):
+        assert stm[r] == (8 if r in bad else 0), (r, stm[r])
+    ok = stm == 0
+    np.testing.assert_array_equal(lpm[ok], lpv[ok])

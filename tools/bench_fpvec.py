@@ -44,6 +44,10 @@ def main():
     ap.add_argument("--shard-chunk", type=int, default=512)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine option for both contexts (prio3gpu_ctx_set_option), repeatable")
+    ap.add_argument("--lopt", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine option for the leader's context only, repeatable")
+    ap.add_argument("--hopt", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine option for the helper's context only, repeatable")
     args = ap.parse_args()
 
     import torch
@@ -73,9 +77,13 @@ def main():
     tiles = B // U if not args.distinct else 1
     vl = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(args.bits, args.entries, vk)
     vh = Prio3Gpu.new_fixedpoint_boundedl2_vec_sum(args.bits, args.entries, vk)
-    opts = dict((o.split("=", 1)[0], int(o.split("=", 1)[1])) for o in args.opt)
-    for v_ in (vl, vh):
-        for k_, val in opts.items():
+    def parse(lst):
+        return dict((o.split("=", 1)[0], int(o.split("=", 1)[1])) for o in lst)
+
+    opts = parse(args.opt)
+    lopts, hopts = {**opts, **parse(args.lopt)}, {**opts, **parse(args.hopt)}
+    for v_, o_ in ((vl, lopts), (vh, hopts)):
+        for k_, val in o_.items():
             v_.set_option(k_, val)
     s = vl.sizes
     shard_info = None
@@ -203,7 +211,7 @@ def main():
            "reports_per_step": B, "unique": B if args.distinct else U,
            "gpu_shard": shard_info, "ms_per_step": dt * 1e3,
            "reports_per_sec": B / dt, "overlap_leader_helper": bool(args.overlap),
-           "engine_options": opts,
+           "engine_options": {"leader": lopts, "helper": hopts},
            "cpu_baseline": {"reports_per_sec": cpu_rate, "threads": args.threads,
                             "kind": "port", "sample": f"{U} reports"},
            "speedup_vs_cpu": (B / dt) / cpu_rate,
