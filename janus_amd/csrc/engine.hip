@@ -670,8 +670,12 @@ int launch_fpv_query_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t
   {
     PROF(KID_FPV_WIRES1);
     if (m1)
-      hipLaunchKernelGGL(k_fpv_wires1_mfma, dim3(N), dim3(256), fpv_w1m_lds(g), c->stream, g, N,
-                         meas, CRows{wrows.base, wrows.stride}, prep, d_status);
+      // tile groups per report: enough blocks to fill the chip at small chunks
+      hipLaunchKernelGGL(k_fpv_wires1_mfma,
+                         dim3(N, std::max<uint32_t>(1u, std::min<uint32_t>(
+                                     4u, (g.bits * g.chunk1 + 127u) / 128u))),
+                         dim3(256), fpv_w1m_lds(g), c->stream, g, N, meas,
+                         CRows{wrows.base, wrows.stride}, prep, d_status);
     else
       hipLaunchKernelGGL(k_fpv_wires1, dim3((g.chunk1 + 255) / 256, N), dim3(256), 0, c->stream, g,
                          N, meas, CRows{wrows.base, wrows.stride}, prep, d_status);

@@ -75,6 +75,15 @@ DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[1
   }
 }
 
+// Timing-only diagnostic builds of k_helper_xof (wrong bytes; tools/build_variant.sh):
+//   1: the storer waves leave at once (the producer does not wait for them)
+//   2: the consumer waves skip their permutation     3: the producer waves skip theirs
+//   4: the producer writes no ring slot               5: the producer stores no snapshot
+#ifndef P3G_DIAG_HX
+#define P3G_DIAG_HX 0
+#endif
+
+
 constexpr uint32_t kHxRows = 64;              // reports per producer/consumer pair (a wave each)
 constexpr uint32_t kHxDepth = 4;              // ring slots: the producer may run 4 blocks ahead
 // LDS ring bytes of one pair (slot rows kHxRows + 1 words apart; see k_helper_xof)
@@ -131,6 +140,10 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
   const uint32_t r0 = (blockIdx.x * kPairs + pair) * kHxRows;
   if (r0 >= n) return;  // a whole pair past the batch (no barrier follows)
   if (cfg.wave_prio) __builtin_amdgcn_s_setprio(3);  // the chain first on its SIMD
+  if (P3G_DIAG_HX == 1 && storer) {
+    *vstor = 0x7FFFFFFFu;
+    return;
+  }
   const uint32_t r = r0 + lane;
   const bool live = r < n && (!status || status[r] == ST_OK);
   const uint32_t rr = r < n ? r : n - 1u;  // every lane runs the loop, clamped row
@@ -167,7 +180,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
     bool perm = true;
     if (producer) {
       const int64_t j0 = 21 * i;
-      if (snaps != nullptr && (i % kSnapEvery) == 0 && r < n) {  // s = the state of block i
+      if (P3G_DIAG_HX != 5 && snaps != nullptr && (i % kSnapEvery) == 0 && r < n) {
         uint64_t* sp = snaps + ((size_t)r * snap_count(cfg) + (size_t)(i / kSnapEvery)) * 25;
 #pragma unroll
         for (int w = 0; w < 25; ++w) sp[w] = s[w];
@@ -175,8 +188,10 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
       while (i - (int64_t)min(*vcons, *vstor) >= (int64_t)kDepth) __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
       uint64_t* slot = ring + (i % kDepth) * kSlot;
+      if (P3G_DIAG_HX != 4) {
 #pragma unroll
-      for (int w = 0; w < 21; ++w) slot[w * kStride + lane] = j0 + w < nd ? s[w] : 0ull;
+        for (int w = 0; w < 21; ++w) slot[w * kStride + lane] = j0 + w < nd ? s[w] : 0ull;
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
       *vprod = (uint32_t)(i + 1);
       perm = 21 * (i + 1) < nd;
@@ -276,6 +291,8 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
         for (int k = 0; k < 6; ++k) carry[k] = 0ull;
       }
     }
+    if (P3G_DIAG_HX == 2 && !producer) perm = false;
+    if (P3G_DIAG_HX == 3 && producer) perm = false;
     if (perm) keccak_x(s, cfg.xof);
   }
   if (storer) {

@@ -193,8 +193,9 @@ k_fpv_wires0_mfma(Cfg cfg, uint32_t n, CRows meas, CRows wrows, const uint8_t* s
 // over the n adjacent lanes of entry j.  Entry widths n that divide a 32-column tile: 16, 32.
 __host__ __device__ inline bool fpv_w1m_bits_ok(uint32_t bits) { return bits == 16 || bits == 32; }
 
-// grid (n), 256 threads: wave = 32-column tile (tiles loop over the waves), K-step q covers calls
-// 2q (lane half 0) and 2q + 1; each half-wave reads 512 contiguous bytes per K-step.
+// grid (n, S), 256 threads: block (r, s) takes the 32-column tiles s nw + wave + k S nw (every
+// block of a report converts the same weights), K-step q covers calls 2q (lane half 0) and 2q + 1;
+// each half-wave reads 512 contiguous bytes per K-step.
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_fpv_wires1_mfma(Cfg cfg, uint32_t n, CRows meas, CRows wrows, Rows prep, const uint8_t* status) {
   using FO = Field128Ops;
@@ -233,7 +234,8 @@ k_fpv_wires1_mfma(Cfg cfg, uint32_t n, CRows meas, CRows wrows, Rows prep, const
     }
   };
   uint4 xv[U];
-  load_batch(wave, 0, xv);  // in flight while the weights are converted
+  const uint32_t t0 = blockIdx.y * nw + wave, tstep = gridDim.y * nw;  // this wave's tiles
+  load_batch(t0, 0, xv);  // in flight while the weights are converted
 
   F128 s0 = FO::zero(), s1 = FO::zero(), s2 = FO::zero();
   for (uint32_t kk = tid; kk < 2 * KQ; kk += blockDim.x) {
@@ -249,12 +251,12 @@ k_fpv_wires1_mfma(Cfg cfg, uint32_t n, CRows meas, CRows wrows, Rows prep, const
   // 2^l (Montgomery) for this lane's bit l = column mod n (tiles start at multiples of n)
   const uint32_t l = nn & (nb - 1u);
   const F128 two_l = FO::to_mont(FO::from_u64x2(1ull << l, 0ull));
-  for (uint32_t tile = wave; tile < NT; tile += nw) {
+  for (uint32_t tile = t0; tile < NT; tile += tstep) {
     i32x16_t acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0;
     for (uint32_t q0 = 0; q0 < KQ; q0 += U) {
-      if (q0 > 0 || tile != wave) load_batch(tile, q0, xv);
+      if (q0 > 0 || tile != t0) load_batch(tile, q0, xv);
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         if (q0 + u < KQ) {
