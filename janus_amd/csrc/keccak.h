@@ -148,7 +148,8 @@ constexpr Xof kXofShake128{1u, 0x1Fu};
 constexpr Xof kXofTurboShake128{0u, 0x01u};
 
 // P3G_KECCAK_ASM: the rounds as generated inline assembly with VGPR-bank-aware registers
-// (keccak_asm.h, tools/gen_keccak_asm.py) instead of keccak_round32 above.
+// (keccak_asm.h, tools/gen_keccak_asm.py) instead of keccak_round32 above; 1 unrolled, 2 a loop
+// of two-round bodies (~3 KB of code per call site instead of ~35 KB).
 #ifndef P3G_KECCAK_ASM
 #define P3G_KECCAK_ASM 0
 #endif
@@ -163,7 +164,9 @@ DEVI void keccak_x(uint64_t a[25], const Xof& x) {
     l[i] = (uint32_t)a[i];
     h[i] = (uint32_t)(a[i] >> 32);
   }
-#if P3G_KECCAK_ASM
+#if P3G_KECCAK_ASM == 2
+  keccak_asm_rolled(l, h, x.full != 0u);
+#elif P3G_KECCAK_ASM
   if (x.full) keccak_asm_rounds_0_12(l, h);
   keccak_asm_rounds_12_24(l, h);
 #else

@@ -109,6 +109,9 @@ def search(seed=1, restarts=24, iters=20000):
     return cost(*best[1]), best[1]
 
 
+ROLL_U = 2  # rounds per body of the rolled loop
+
+
 def allocate(banks_a, banks_c, banks_r, banks_b, base):
     """Physical registers for one half: A[25], then a pool T holding C[5], R[5] during theta and
     B[1..24] afterwards (a B value may take a dead C / R register of its bank)."""
@@ -137,8 +140,9 @@ def allocate(banks_a, banks_c, banks_r, banks_b, base):
     return A, C, R, B, used
 
 
-def round_asm(R_, lo, hi):
-    """Instructions of round R_ (lo / hi: dicts of register lists A, C, R, B)."""
+def round_asm(R_, lo, hi, iota=True):
+    """Instructions of round R_ (lo / hi: dicts of register lists A, C, R, B); iota=False leaves
+    the round constant to the caller (the rolled loop xors it from SGPRs)."""
     ins = []
     v = lambda n: "v%d" % n
     # theta parities: first all 3-input halves, then the rest (the second reads the first)
@@ -184,6 +188,8 @@ def round_asm(R_, lo, hi):
                     v(half["A"][x + 5 * y]), v(Bx[x + 5 * y]), v(Bx[(x + 1) % 5 + 5 * y]),
                     v(Bx[(x + 2) % 5 + 5 * y])))
     rc = RC[R_]
+    if not iota:
+        return ins
     if rc & 0xFFFFFFFF:
         ins.append("v_xor_b32 %s, 0x%x, %s" % (v(lo["A"][0]), rc & 0xFFFFFFFF, v(lo["A"][0])))
     if rc >> 32:
@@ -228,6 +234,38 @@ def main():
             ops.append('"+{v%d}"(h[%d])' % (hi_A[i], i))
         out.append("      : " + ",\n        ".join(", ".join(ops[k:k + 5]) for k in range(0, 50, 5)) + "\n")
         out.append("      :\n      : P3G_KECCAK_ASM_CLOBBERS);\n}\n\n")
+    # rolled form: every round uses the same registers, so one loop body of ROLL_U rounds serves
+    # all 24 (or TurboSHAKE's last 12); the round constants come from a device table by scalar
+    # loads issued at the top of the body.  ~3 KB of code instead of ~35 KB unrolled.
+    out.append("__device__ const uint64_t p3g_keccak_rc[24] = {\n")
+    for k in range(0, 24, 4):
+        out.append("    " + ", ".join("0x%016xull" % x for x in RC[k:k + 4]) + ",\n")
+    out.append("};\n\n")
+    U = ROLL_U
+    out.append("// nr = 24 (Keccak-f) or 12 (its last 12 rounds); nr %% %d == 0\n" % U)
+    out.append("__device__ __forceinline__ void keccak_asm_rolled(uint32_t l[25], uint32_t h[25], bool full) {\n")
+    out.append("  const uint64_t* t = full ? p3g_keccak_rc : p3g_keccak_rc + 12;\n")
+    out.append("  const uint32_t iters = (full ? 24u : 12u) / %du;\n" % U)
+    body = ["s_mov_b64 s[90:91], %[t]", "s_mov_b32 s92, %[it]", "L_keccak_%=:"]
+    body.append("s_load_dwordx%d s[80:%d], s[90:91], 0x0" % (2 * U, 80 + 2 * U - 1))
+    for u in range(U):
+        body += round_asm(0, lo, hi, iota=False)
+        if u == 0:
+            body.append("s_waitcnt lgkmcnt(0)")
+        body.append("v_xor_b32 v%d, s%d, v%d" % (lo_A[0], 80 + 2 * u, lo_A[0]))
+        body.append("v_xor_b32 v%d, s%d, v%d" % (hi_A[0], 81 + 2 * u, hi_A[0]))
+    body += ["s_add_u32 s90, s90, %d" % (8 * U), "s_addc_u32 s91, s91, 0", "s_sub_u32 s92, s92, 1",
+             "s_cmp_lg_u32 s92, 0", "s_cbranch_scc1 L_keccak_%="]
+    out.append("  asm volatile(\n")
+    for k, line in enumerate(body):
+        sep = "\\n\\t" if k + 1 < len(body) else ""
+        if line.endswith(":"):
+            sep = "\\n"
+        out.append('      "%s%s"\n' % (line, sep))
+    out.append("      : " + ",\n        ".join(", ".join(ops[k:k + 5]) for k in range(0, 50, 5)) + "\n")
+    sg = ", ".join('"s%d"' % k for k in list(range(80, 80 + 2 * U)) + [90, 91, 92])
+    out.append("      : [t] \"s\"(t), [it] \"s\"(iters)\n")
+    out.append("      : P3G_KECCAK_ASM_CLOBBERS, %s, \"scc\");\n}\n" % sg)
     text = "".join(out)
     if "--check" in sys.argv:
         cur = open(OUT).read() if os.path.exists(OUT) else ""
@@ -302,6 +340,66 @@ def interpret(text, l, h):
     return l, h
 
 
+def interpret_rolled(text, l, h, full=True):
+    """Run keccak_asm_rolled's loop body on a register file (round constants from RC)."""
+    import re
+    m = re.search(r"keccak_asm_rolled\(.*?asm volatile\((.*?)\s*:\s*(\"\+\{.*?)\s*:\s*\[t\]", text, re.S)
+    body, ops = m.group(1), m.group(2)
+    regs = [int(x) for x in re.findall(r'"\+\{v(\d+)\}"', ops)]
+    reg = {}
+    for i in range(25):
+        reg[regs[i]] = l[i]
+        reg[regs[25 + i]] = h[i]
+    lines = [x.replace("\\n\\t", "").replace("\\n", "").strip() for x in re.findall(r'"([^"]*)"', body)]
+    start = [k for k, x in enumerate(lines) if x.startswith("L_keccak")][0] + 1
+    loop = lines[start:]
+    r0 = 0 if full else 12
+    M32 = 0xFFFFFFFF
+    for it in range((24 - r0) // ROLL_U):
+        sg = {}
+        for k in range(ROLL_U):
+            rc = RC[r0 + it * ROLL_U + k]
+            sg[80 + 2 * k], sg[81 + 2 * k] = rc & M32, rc >> 32
+        for line in loop:
+            if not line.startswith("v_"):
+                continue
+            op, rest = line.split(" ", 1)
+            args = [x.strip() for x in rest.replace(" bitop3:", ", bitop3:").split(",")]
+
+            def val(t):
+                if t.startswith("v"):
+                    return reg[int(t[1:])]
+                if t.startswith("s"):
+                    return sg[int(t[1:])]
+                return int(t, 0)
+            d = int(args[0][1:])
+            if op == "v_bitop3_b32":
+                a_, b_, c_ = val(args[1]), val(args[2]), val(args[3])
+                lut = int(args[4].split(":")[1], 0)
+                r = 0
+                for bit in range(32):
+                    idx = (((a_ >> bit) & 1) << 2) | (((b_ >> bit) & 1) << 1) | ((c_ >> bit) & 1)
+                    r |= ((lut >> idx) & 1) << bit
+                reg[d] = r
+            elif op == "v_alignbit_b32":
+                hi_, lo_, s = val(args[1]), val(args[2]), int(args[3])
+                reg[d] = (((hi_ << 32) | lo_) >> s) & M32
+            elif op == "v_xor_b32":
+                reg[d] = val(args[1]) ^ val(args[2])
+            else:
+                raise ValueError(op)
+    return [reg[regs[i]] for i in range(25)], [reg[regs[25 + i]] for i in range(25)]
+
+
+def selftest_rolled(path=OUT, seed=7):
+    rng = random.Random(seed)
+    a = [rng.getrandbits(64) for _ in range(25)]
+    l, h = [x & 0xFFFFFFFF for x in a], [x >> 32 for x in a]
+    l, h = interpret_rolled(open(path).read(), l, h)
+    got = [(hh << 32) | ll for ll, hh in zip(l, h)]
+    return got == keccak_f_ref(a)
+
+
 def selftest(path=OUT, seed=7):
     rng = random.Random(seed)
     a = [rng.getrandbits(64) for _ in range(25)]
@@ -312,6 +410,6 @@ def selftest(path=OUT, seed=7):
 
 
 if __name__ == "__main__" and "--selftest" in sys.argv:
-    ok = selftest()
+    ok = selftest() and selftest_rolled()
     print("selftest", "ok" if ok else "MISMATCH")
     sys.exit(0 if ok else 1)
