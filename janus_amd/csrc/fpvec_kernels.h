@@ -84,6 +84,42 @@ DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[1
 #endif
 
 
+// Ring counters in LDS.  kLds: read and written with ds instructions; else through a volatile
+// generic pointer, which compiles to FLAT (sc0 sc1) with an s_waitcnt vmcnt(0) lgkmcnt(0) that
+// also waits for every global access the wave has in flight.  LDS operations of one wave complete
+// in order, so a counter written after a slot's data publishes that data.  Measured at 10,240
+// config E reports (profiles/r05/fpvec2/r5_ctr_*.log): the helper's chains run 1,383 -> 1,277 ms
+// alone and 1,469 -> 1,306 beside the leader with ds counters, while the leader's k_jr_ring goes
+// 1,234 -> 1,371 and 1,314 -> 1,486 -- so k_helper_xof takes ds counters (P3G_HX_CTR_LDS) and
+// k_jr_ring keeps the FLAT form (P3G_JR_CTR_LDS).
+#ifndef P3G_HX_CTR_LDS
+#define P3G_HX_CTR_LDS 1
+#endif
+#ifndef P3G_JR_CTR_LDS
+#define P3G_JR_CTR_LDS 0
+#endif
+constexpr bool kHxLds = P3G_HX_CTR_LDS != 0, kJrLds = P3G_JR_CTR_LDS != 0;
+template <bool kLds>
+DEVI uint32_t ctr_ld(uint32_t* p) {
+  if constexpr (!kLds) {
+    return *reinterpret_cast<volatile uint32_t*>(p);
+  } else {
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)p;
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return __builtin_amdgcn_readfirstlane(v);
+  }
+}
+template <bool kLds>
+DEVI void ctr_st(uint32_t* p, uint32_t v) {
+  if constexpr (!kLds) {
+    *reinterpret_cast<volatile uint32_t*>(p) = v;
+  } else {
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)p;
+    asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
+  }
+}
+
 constexpr uint32_t kHxRows = 64;              // reports per producer/consumer pair (a wave each)
 constexpr uint32_t kHxDepth = 4;              // ring slots: the producer may run 4 blocks ahead
 // LDS ring bytes of one pair (slot rows kHxRows + 1 words apart; see k_helper_xof)
@@ -130,9 +166,9 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
   const uint32_t wave = threadIdx.x / kHxRows;  // wave-uniform roles
   const uint32_t pair = wave % kPairs, role = wave / kPairs;
   uint64_t* ring = hx_dyn + (size_t)pair * (kDepth * kSlot);
-  volatile uint32_t* vprod = &counters[3 * pair];
-  volatile uint32_t* vcons = &counters[3 * pair + 1];
-  volatile uint32_t* vstor = &counters[3 * pair + 2];
+  uint32_t* vprod = &counters[3 * pair];
+  uint32_t* vcons = &counters[3 * pair + 1];
+  uint32_t* vstor = &counters[3 * pair + 2];
   if (threadIdx.x < 3 * kPairs) counters[threadIdx.x] = 0u;
   __syncthreads();
   // role 0 produces, role 1 consumes, role 2 stores the expanded share to HBM / sums its columns
@@ -141,7 +177,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
   if (r0 >= n) return;  // a whole pair past the batch (no barrier follows)
   if (cfg.wave_prio) __builtin_amdgcn_s_setprio(3);  // the chain first on its SIMD
   if (P3G_DIAG_HX == 1 && storer) {
-    *vstor = 0x7FFFFFFFu;
+    ctr_st<kHxLds>(vstor, 0x7FFFFFFFu);
     return;
   }
   const uint32_t r = r0 + lane;
@@ -185,7 +221,8 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
 #pragma unroll
         for (int w = 0; w < 25; ++w) sp[w] = s[w];
       }
-      while (i - (int64_t)min(*vcons, *vstor) >= (int64_t)kDepth) __builtin_amdgcn_s_sleep(1);
+      while (i - (int64_t)min(ctr_ld<kHxLds>(vcons), ctr_ld<kHxLds>(vstor)) >= (int64_t)kDepth)
+        __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
       uint64_t* slot = ring + (i % kDepth) * kSlot;
       if (P3G_DIAG_HX != 4) {
@@ -193,12 +230,12 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
         for (int w = 0; w < 21; ++w) slot[w * kStride + lane] = j0 + w < nd ? s[w] : 0ull;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
-      *vprod = (uint32_t)(i + 1);
+      ctr_st<kHxLds>(vprod, (uint32_t)(i + 1));
       perm = 21 * (i + 1) < nd;
     } else if (storer) {
       // store block i of the expanded share and check its elements are canonical
       const int64_t j0 = 21 * i;
-      while ((int64_t)*vprod <= i) __builtin_amdgcn_s_sleep(1);
+      while ((int64_t)ctr_ld<kHxLds>(vprod) <= i) __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
       const uint64_t* slot = ring + (i % kDepth) * kSlot;
 #pragma unroll
@@ -216,7 +253,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
-      *vstor = (uint32_t)(i + 1);
+      ctr_st<kHxLds>(vstor, (uint32_t)(i + 1));
       if (spec_lo != nullptr) {
         uint32_t l32 = 0, h32 = 0, cy = 0;
 #pragma unroll
@@ -270,7 +307,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
       const bool data = 21 * b < nd;  // else the block is past the share: zeros
       uint64_t A[16];
       if (data) {
-        while ((int64_t)*vprod <= b) __builtin_amdgcn_s_sleep(1);
+        while ((int64_t)ctr_ld<kHxLds>(vprod) <= b) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         const uint64_t* slot = ring + (b % kDepth) * kSlot;
 #pragma unroll
@@ -285,7 +322,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kStride + lane];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
-        *vcons = (uint32_t)(b + 1);
+        ctr_st<kHxLds>(vcons, (uint32_t)(b + 1));
       } else {
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = 0ull;
@@ -394,8 +431,8 @@ __global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint3
   const uint32_t pair = wave % kPairs;
   const bool loader = wave >= kPairs;  // waves 0..kPairs-1: sponges, then the loaders
   uint64_t* ring = jr_dyn + (size_t)pair * (kHxDepth * kSlot);
-  volatile uint32_t* vprod = &counters[2 * pair];
-  volatile uint32_t* vcons = &counters[2 * pair + 1];
+  uint32_t* vprod = &counters[2 * pair];
+  uint32_t* vcons = &counters[2 * pair + 1];
   if (threadIdx.x < 2 * kPairs) counters[threadIdx.x] = 0u;
   __syncthreads();
   const uint32_t r0 = (blockIdx.x * kPairs + pair) * kHxRows;
@@ -446,7 +483,8 @@ __global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint3
 #pragma unroll
         for (int w = 0; w < 21; ++w) s[w] = j0 + w < nd ? ld64(src + 8 * w) : 0ull;
       }
-      while (i - (int64_t)*vcons >= (int64_t)kHxDepth) __builtin_amdgcn_s_sleep(1);
+      while (i - (int64_t)ctr_ld<kJrLds>(vcons) >= (int64_t)kHxDepth)
+        __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
       uint64_t* slot = ring + (i % kHxDepth) * kSlot;
 #pragma unroll
@@ -463,14 +501,14 @@ __global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint3
         spec_cy[at] = (uint8_t)cy;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
-      *vprod = (uint32_t)(i + 1);
+      ctr_st<kJrLds>(vprod, (uint32_t)(i + 1));
       perm = false;
     } else {
       const int64_t b = i;
       const bool has = 21 * b < nd;  // else the block is past the share: zeros
       uint64_t A[16];
       if (has) {
-        while ((int64_t)*vprod <= b) __builtin_amdgcn_s_sleep(1);
+        while ((int64_t)ctr_ld<kJrLds>(vprod) <= b) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         const uint64_t* slot = ring + (b % kHxDepth) * kSlot;
 #pragma unroll
@@ -485,7 +523,7 @@ __global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint3
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kJrRingStride + lane];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
-        *vcons = (uint32_t)(b + 1);
+        ctr_st<kJrLds>(vcons, (uint32_t)(b + 1));
       } else {
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = 0ull;
