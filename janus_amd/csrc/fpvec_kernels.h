@@ -99,6 +99,28 @@ DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[1
 #define P3G_JR_CTR_LDS 0
 #endif
 constexpr bool kHxLds = P3G_HX_CTR_LDS != 0, kJrLds = P3G_JR_CTR_LDS != 0;
+// A/B split of k_jr_ring's counter accesses by wave and direction (default: all kJrLds)
+#ifndef P3G_JR_LOADER_LDS
+#define P3G_JR_LOADER_LDS P3G_JR_CTR_LDS
+#endif
+#ifndef P3G_JR_SPONGE_LD_LDS
+#define P3G_JR_SPONGE_LD_LDS P3G_JR_CTR_LDS
+#endif
+#ifndef P3G_JR_SPONGE_ST_LDS
+#define P3G_JR_SPONGE_ST_LDS P3G_JR_CTR_LDS
+#endif
+constexpr bool kJrLoaderLds = P3G_JR_LOADER_LDS != 0, kJrSpongeLdLds = P3G_JR_SPONGE_LD_LDS != 0,
+               kJrSpongeStLds = P3G_JR_SPONGE_ST_LDS != 0;
+#ifndef P3G_HX_CONS_ST_LDS  // A/B: k_helper_xof's consumer / producer publish
+#define P3G_HX_CONS_ST_LDS P3G_HX_CTR_LDS
+#endif
+#ifndef P3G_HX_PROD_ST_LDS
+#define P3G_HX_PROD_ST_LDS P3G_HX_CTR_LDS
+#endif
+constexpr bool kHxConsStLds = P3G_HX_CONS_ST_LDS != 0, kHxProdStLds = P3G_HX_PROD_ST_LDS != 0;
+#ifndef P3G_JR_LOADER_SLEEP
+#define P3G_JR_LOADER_SLEEP 1  // A/B: s_sleep quanta of k_jr_ring's loader while the ring is full
+#endif
 template <bool kLds>
 DEVI uint32_t ctr_ld(uint32_t* p) {
   if constexpr (!kLds) {
@@ -230,7 +252,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
         for (int w = 0; w < 21; ++w) slot[w * kStride + lane] = j0 + w < nd ? s[w] : 0ull;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
-      ctr_st<kHxLds>(vprod, (uint32_t)(i + 1));
+      ctr_st<kHxProdStLds>(vprod, (uint32_t)(i + 1));
       perm = 21 * (i + 1) < nd;
     } else if (storer) {
       // store block i of the expanded share and check its elements are canonical
@@ -322,7 +344,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kStride + lane];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
-        ctr_st<kHxLds>(vcons, (uint32_t)(b + 1));
+        ctr_st<kHxConsStLds>(vcons, (uint32_t)(b + 1));
       } else {
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = 0ull;
@@ -483,8 +505,8 @@ __global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint3
 #pragma unroll
         for (int w = 0; w < 21; ++w) s[w] = j0 + w < nd ? ld64(src + 8 * w) : 0ull;
       }
-      while (i - (int64_t)ctr_ld<kJrLds>(vcons) >= (int64_t)kHxDepth)
-        __builtin_amdgcn_s_sleep(1);
+      while (i - (int64_t)ctr_ld<kJrLoaderLds>(vcons) >= (int64_t)kHxDepth)
+        __builtin_amdgcn_s_sleep(P3G_JR_LOADER_SLEEP);
       asm volatile("" ::: "memory");
       uint64_t* slot = ring + (i % kHxDepth) * kSlot;
 #pragma unroll
@@ -501,14 +523,14 @@ __global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint3
         spec_cy[at] = (uint8_t)cy;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
-      ctr_st<kJrLds>(vprod, (uint32_t)(i + 1));
+      ctr_st<kJrLoaderLds>(vprod, (uint32_t)(i + 1));
       perm = false;
     } else {
       const int64_t b = i;
       const bool has = 21 * b < nd;  // else the block is past the share: zeros
       uint64_t A[16];
       if (has) {
-        while ((int64_t)ctr_ld<kJrLds>(vprod) <= b) __builtin_amdgcn_s_sleep(1);
+        while ((int64_t)ctr_ld<kJrSpongeLdLds>(vprod) <= b) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         const uint64_t* slot = ring + (b % kHxDepth) * kSlot;
 #pragma unroll
@@ -523,7 +545,7 @@ __global__ void __launch_bounds__(2 * kHxRows * kPairs) k_jr_ring(Cfg cfg, uint3
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kJrRingStride + lane];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
-        ctr_st<kJrLds>(vcons, (uint32_t)(b + 1));
+        ctr_st<kJrSpongeStLds>(vcons, (uint32_t)(b + 1));
       } else {
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = 0ull;
