@@ -144,6 +144,11 @@ DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 #ifndef P3G_DIAG_FW_NOLOAD
 #define P3G_DIAG_FW_NOLOAD 0
 #endif
+//   P3G_DIAG_FW_PHASE        k_flp_weights without the products of one phase (1 forward prefix,
+//                            2 Horner, 3 backward) -- where its time goes
+#ifndef P3G_DIAG_FW_PHASE
+#define P3G_DIAG_FW_PHASE 0
+#endif
 
 template <>
 struct SqueezeVec<Field128Ops> {
@@ -1537,7 +1542,12 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
     if (k <= C && ((k - 1u) & 7u) == 0u) FO::store(S((k - 1u) >> 3), P);
     const T d = FO::sub(tm, ld_tw<FO>(cfg, k <= C ? k : 1u));
     T nP, nrp;
+#if P3G_DIAG_FW_PHASE == 1  // timing only: no forward products
+    nP = FO::add(P, d);
+    nrp = FO::add(rp, rm);
+#else
     mont_mul2(P, d, nP, rp, rm, nrp);
+#endif
     if (k <= C) P = nP;
     if (k <= c) {
       rp = nrp;
@@ -1578,7 +1588,13 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
         c1 = xb[u];
       } else {
         T n2, n1, n0;
+#if P3G_DIAG_FW_PHASE == 2  // timing only: no Horner products
+        n2 = FO::add(A2, t3);
+        n1 = FO::add(A1, t3);
+        n0 = FO::add(A0, t3);
+#else
         mul3<FO>(A2, t3, A1, t3, A0, t3, n2, n1, n0);
+#endif
         A2 = FO::add(n2, c2);
         A1 = FO::add(n1, c1);
         A0 = FO::add(n0, xb[u]);
@@ -1638,7 +1654,15 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
         // the chain step {inv pt_k, inv d_k}, the next entry's P_(k-2) alpha^(k-1)/m,
         // q <- q / r^c, and MM of the previous entry (k + 1)
         T lk, ninv, nptw, nq, mmp;
+#if P3G_DIAG_FW_PHASE == 3  // timing only: no backward products
+        lk = FO::add(inv, ptw);
+        ninv = FO::add(inv, d);
+        nptw = FO::add(pn, tn);
+        nq = FO::add(q, rcinv);
+        mmp = FO::add(lkp, qp);
+#else
         mont_mul5(inv, ptw, lk, inv, d, ninv, pn, tn, nptw, q, rcinv, nq, lkp, qp, mmp);
+#endif
         if ((uint32_t)u + 1u < nb) emit_mm((uint32_t)u + 1u, mmp);
         inv = ninv;
         ptw = nptw;
