@@ -20,6 +20,7 @@
 #include "fpvec_kernels.h"
 #include "wires_mfma.h"
 #include "fpvec_mfma.h"
+#include "fpvec_pair.h"
 
 using namespace p3g;
 
@@ -215,6 +216,9 @@ struct prio3gpu_ctx {
   // launch takes at most half the CUs, else 2, so a leader and a helper launch side by side
   // still give every sponge wave its own SIMD)
   uint32_t chain_pairs = 0;
+  // "pair_chains": the FixedPoint chains with each sponge state on a lane pair (fpvec_pair.h:
+  // k_helper_xof_pair, k_jr_ring_pair; half the instructions on the latency-bound chain)
+  bool pair_chains = true;
   // "query_overlap": snapshot-mode helper query regenerates half-chunk i+1 on a second stream
   // while half-chunk i is queried (two scratch halves; 0, the default: regenerate and query in
   // turn -- measured faster: the VALU-bound regeneration starves the co-running wire passes)
@@ -286,6 +290,7 @@ struct prio3gpu_state {
   // meas_rows goes through regen_rows.
   DevBuf snaps, scratch;
   bool snap = false, snap_active = false;
+  bool snap_pair = false;  // the snapshots were written by k_helper_xof_pair (dword-pair halves)
   CRows meas_rows{nullptr, 0};  // measurement shares of the prepared batch
   CRows proof_rows{nullptr, 0};  // proof shares (prepare_init_xof -> prepare_init_query)
   bool xof_done = false;         // the XOF phase ran; the query phase is due
@@ -598,7 +603,8 @@ int regen_rows(prio3gpu_ctx* c, prio3gpu_state* st, size_t r0, size_t nr, uint8_
   if (!strm) strm = c->stream;
   const uint64_t lanes = (uint64_t)nr * snap_count(g);
   PROF_ON(KID_FPV_REGEN, strm);
-  hipLaunchKernelGGL(k_fpv_regen, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, strm, g,
+  hipLaunchKernelGGL(st->snap_pair ? k_fpv_regen<true> : k_fpv_regen<false>,
+                     dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, strm, g,
                      (uint32_t)nr, (uint32_t)r0, reinterpret_cast<const uint64_t*>(st->snaps.p),
                      Rows{dst, row});
   HIPCHK(hipGetLastError());
@@ -824,7 +830,19 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
         CHK(c->fallback.ensure(4));
         uint32_t* fb = reinterpret_cast<uint32_t*>(c->fallback.p);
         HIPCHK(hipMemsetAsync(fb, 0, 4, c->stream));
-        {
+        st->snap_pair = c->pair_chains;
+        if (c->pair_chains) {
+          // 64 reports per workgroup: two producer, two consumer sponge waves and a storer
+          PROF(KID_HELPER_XOF);
+          const uint32_t blocks = (N + kHxRows - 1) / kHxRows;
+          const size_t lds = std::max<size_t>(kHxPairLds, spread_ok(c, blocks) ? c->spread_lds : 0);
+          hipLaunchKernelGGL(k_helper_xof_pair<kHxDepth>, dim3(blocks), dim3(5 * kHxRows), lds,
+                             c->stream, g, N, CRows{d_in, in_pitch}, nonces, pub, mo, po,
+                             Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
+                             Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, fb,
+                             spec_lo, spec_cy,
+                             st->snap ? reinterpret_cast<uint64_t*>(st->snaps.p) : nullptr);
+        } else {
           PROF(KID_HELPER_XOF);
           const uint32_t P = chain_pairs(c, n), rows = P * kHxRows;
           const uint32_t blocks = (N + rows - 1) / rows;
@@ -880,8 +898,19 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
     // few huge FixedPoint reports: sponge wave + loader wave per CU (k_jr_ring)
     const uint32_t P = chain_pairs(c, n), rows = P * kHxRows;
     const uint32_t blocks = (N + rows - 1) / rows;
-    if (g.jr_len > 0 && g.kind == KIND_FPVEC && c->jr_ring && c->jr_lds == 0 &&
-        spread_ok(c, blocks)) {
+    const uint32_t pblocks = (N + 2 * kHxRows - 1) / (2 * kHxRows);
+    if (g.jr_len > 0 && g.kind == KIND_FPVEC && c->jr_ring && c->jr_lds == 0 && c->pair_chains &&
+        spread_ok(c, pblocks)) {
+      // 128 reports per workgroup: four sponge waves (a lane pair per report) and two loaders
+      PROF(KID_JR_RING);
+      const size_t lds = std::max<size_t>(kJrPairLds, c->spread_lds);
+      hipLaunchKernelGGL(k_jr_ring_pair, dim3(pblocks), dim3(6 * kHxRows), lds, c->stream,
+                         g, N, (uint32_t)st->agg_id, nonces, pub, blinds, meas,
+                         Rows{st->part.u8(), 16}, Rows{st->seed.u8(), 16},
+                         Rows{st->jr.u8(), (size_t)g.jr_len * es}, d_status, spec_lo, spec_cy);
+      ring_done = true;
+    } else if (g.jr_len > 0 && g.kind == KIND_FPVEC && c->jr_ring && c->jr_lds == 0 &&
+               spread_ok(c, blocks)) {
       PROF(KID_JR_RING);
       const size_t lds = std::max<size_t>(P * kHxRingBytes, c->spread_lds);
       auto kern = P == 2 ? k_jr_ring<2> : k_jr_ring<1>;
@@ -1861,6 +1890,8 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
       return PRIO3GPU_E_ARG;
     }
     c->chain_pairs = (uint32_t)value;
+  } else if (k == "pair_chains") {
+    c->pair_chains = on;
   } else if (k == "wires_mfma") {
     c->wires_mfma = on;
   } else if (k == "wires_cols") {

@@ -23,6 +23,7 @@
 //   k_fpv_decide    block per report
 #pragma once
 #include "prio3_kernels.h"
+#include "keccak_pair.h"
 
 namespace p3g {
 
@@ -387,6 +388,8 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
 // of `out` from k_helper_xof's state snapshots: lane = (report, snapshot), each lane stores its
 // kSnapEvery blocks exactly as the storer wave would have (the share is the raw XOF stream; the
 // fused path checked every element canonical) and permutes between them.
+// kPair: the snapshots hold (even half, odd half) dword pairs (k_helper_xof_pair, fpvec_pair.h).
+template <bool kPair>
 __global__ void __launch_bounds__(256) k_fpv_regen(Cfg cfg, uint32_t nr, uint32_t r0,
                                                    const uint64_t* snaps, Rows out) {
   const uint32_t nsnap = snap_count(cfg);
@@ -397,7 +400,10 @@ __global__ void __launch_bounds__(256) k_fpv_regen(Cfg cfg, uint32_t nr, uint32_
   const uint64_t* sp = snaps + ((size_t)(r0 + q) * nsnap + k) * 25;
   uint64_t s[25];
 #pragma unroll
-  for (int w = 0; w < 25; ++w) s[w] = sp[w];
+  for (int w = 0; w < 25; ++w) {
+    const uint64_t v = sp[w];
+    s[w] = kPair ? kp_zip((uint32_t)v, (uint32_t)(v >> 32)) : v;
+  }
   uint8_t* om = out.at(q);
   const int64_t i0 = (int64_t)k * kSnapEvery;
   const int64_t i1 = i0 + kSnapEvery < nprod ? i0 + kSnapEvery : nprod;

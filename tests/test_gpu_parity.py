@@ -453,10 +453,12 @@ def test_fpvec_helper_two_pass_path_bit_exact(name):
 
 
 @pytest.mark.parametrize("opts", [{}, {"snap_chunk": 1}, {"snap_chunk": 5}, {"helper_snap": 0},
-                                  {"chain_pairs": 2}, {"snap_chunk": 5, "query_overlap": 1},
-                                  {"snap_chunk": 1, "query_overlap": 1}],
+                                  {"pair_chains": 0, "chain_pairs": 2},
+                                  {"snap_chunk": 5, "query_overlap": 1},
+                                  {"snap_chunk": 1, "query_overlap": 1},
+                                  {"pair_chains": 0}, {"pair_chains": 0, "helper_snap": 0}],
                          ids=["snap", "snap_chunk1", "snap_chunk5", "rows", "pairs2", "overlap5",
-                              "overlap1"])
+                              "overlap1", "unpaired", "unpaired_rows"])
 @pytest.mark.parametrize("name", ["fp16_3", "fp64_4", "fp16_300"])
 def test_fpvec_helper_snapshot_mode(name, opts):
     """Snapshot mode (helper_snap, the default): the FixedPoint helper keeps k_helper_xof's sponge
@@ -505,15 +507,21 @@ def test_fpvec_helper_snapshot_whole_waves():
     assert aggs[0] == aggs[1] == expected_aggregate(b, "helper")
 
 
-@pytest.mark.parametrize("pairs", [1, 2])
-def test_fpvec_chain_pairs(pairs):
+@pytest.mark.parametrize("pairs,n", [(1, 100), (2, 100), (0, 100), (0, 161)],
+                         ids=["pairs1", "pairs2", "lane_pairs", "lane_pairs_161"])
+def test_fpvec_chain_pairs(pairs, n):
     """k_helper_xof / k_jr_ring with one or two 64-report chains per workgroup (option
-    chain_pairs): 100 reports, so the second workgroup's pair is partial and, with two pairs, the
-    first workgroup's second pair too.  Both aggregators' prep shares, the prep messages and both
-    aggregates (the chains' column sums) equal the oracle's."""
-    b = make_batch("fp16_3", 100)
+    chain_pairs, pair_chains 0): 100 reports, so the second workgroup's pair is partial and, with
+    two pairs, the first workgroup's second pair too; and the lane-pair kernels (pairs = 0 here:
+    k_helper_xof_pair, 64 reports per workgroup, k_jr_ring_pair, 128) with 100 and 161 reports
+    (161 = a last helper workgroup of 33: one full and one 1-report sponge wave).  Both
+    aggregators' prep shares, the prep messages and both aggregates (the chains' column sums)
+    equal the oracle's."""
+    b = make_batch("fp16_3", n)
     v = gpu_vdaf(b)
-    v.set_option("chain_pairs", pairs)
+    if pairs:
+        v.set_option("pair_chains", 0)
+        v.set_option("chain_pairs", pairs)
     ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
     lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
     assert (lst == 0).all()
@@ -527,8 +535,9 @@ def test_fpvec_chain_pairs(pairs):
     assert hagg.read(0) == expected_aggregate(b, "helper")
 
 
-@pytest.mark.parametrize("opts", [{}, {"jr_ring": 0}, {"spread": 0}, {"chain_pairs": 2}],
-                         ids=["ring", "k_jr_spread", "k_jr_packed", "ring_pairs2"])
+@pytest.mark.parametrize("opts", [{}, {"jr_ring": 0}, {"spread": 0},
+                                  {"pair_chains": 0, "chain_pairs": 2}, {"pair_chains": 0}],
+                         ids=["ring", "k_jr_spread", "k_jr_packed", "ring_pairs2", "ring_unpaired"])
 @pytest.mark.parametrize("name", ["fp16_3", "fp16_300"])
 def test_fpvec_leader_jr_variants(name, opts):
     """The leader's FixedPoint joint-rand part runs k_jr_ring (sponge wave + loader wave writing
