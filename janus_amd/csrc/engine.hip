@@ -1904,7 +1904,11 @@ int prio3gpu_ctx_set_option(prio3gpu_ctx* c, const char* name, int64_t value) {
     }
     (k == "expand_lds" ? c->expand_lds : c->jr_lds) = (size_t)value;
   } else if (k == "wave_prio") {
-    c->cfg.wave_prio = on ? 1u : 0u;
+    if (value < 0 || value > 2) {
+      set_err("option wave_prio: %lld is not 0, 1 or 2", (long long)value);
+      return PRIO3GPU_E_ARG;
+    }
+    c->cfg.wave_prio = (uint32_t)value;
   } else if (k == "exact_squeeze") {
     // every XOF squeeze takes the exact per-element rejection path (test switch); the FixedPoint
     // helper then runs its exact two-pass XOF

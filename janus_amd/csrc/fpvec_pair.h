@@ -18,6 +18,19 @@
 
 namespace p3g {
 
+// Ring counters of k_jr_ring_pair through ds instructions (ctr_ld / ctr_st): its leader chains
+// ran 1,037 -> 975 ms at 10,752 reports against the FLAT form k_jr_ring keeps
+// (profiles/r05/pair/r5_pair5).
+#ifndef P3G_JRP_CTR_LDS
+#define P3G_JRP_CTR_LDS 1
+#endif
+constexpr bool kJrpLds = P3G_JRP_CTR_LDS != 0;
+// Timing-only diagnostic builds of k_jr_ring_pair (wrong bytes): 1 the loader sums no columns,
+// 2 the loader writes the raw word halves instead of unzipping them
+#ifndef P3G_DIAG_JRP
+#define P3G_DIAG_JRP 0
+#endif
+
 constexpr uint32_t kPrRows = 32;                 // reports per sponge wave (two lanes each)
 constexpr uint32_t kPrStride = 65;               // ring row pitch (dwords): conflict-free columns
 constexpr uint32_t kPrSlot = 21 * kPrStride;     // dwords per ring slot
@@ -142,8 +155,9 @@ __global__ void __launch_bounds__(5 * kHxRows) k_helper_xof_pair(Cfg cfg, uint32
   __syncthreads();
   const uint32_t r0 = blockIdx.x * kHxRows;
   if (r0 >= n) return;
-  if (cfg.wave_prio) __builtin_amdgcn_s_setprio(3);
   const bool producer = wave < 2u, storer = wave == 4u;
+  // wave_prio 1: the sponge waves first on their SIMDs (the storer shares one); 2: every wave
+  if (cfg.wave_prio == 2u || (cfg.wave_prio == 1u && !storer)) __builtin_amdgcn_s_setprio(3);
   const uint32_t h = wave & 1u;  // the sponge waves' ring
   const uint32_t p = lane & 1u;
   const KpLane ln = kp_lane(p);
@@ -318,8 +332,8 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
   __syncthreads();
   const uint32_t rb = blockIdx.x * (2 * kHxRows);
   if (rb >= n) return;
-  if (cfg.wave_prio) __builtin_amdgcn_s_setprio(3);
   const bool loader = wave >= 4u;
+  if (cfg.wave_prio == 2u || (cfg.wave_prio == 1u && !loader)) __builtin_amdgcn_s_setprio(3);
   const uint32_t L = loader ? wave & 1u : wave >> 1;  // the 64-row group (a loader's, a sponge's)
   // a group wholly past the batch: its loader and both its sponges leave (no spec column-sum
   // group exists for it); a partial group runs on clamped rows like k_jr_ring
@@ -385,9 +399,16 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
       }
       uint32_t he[21], ho[21];
 #pragma unroll
-      for (int w = 0; w < 21; ++w) kp_unzip(x[w], he[w], ho[w]);
-      while (i - (int64_t)min(ctr_ld<kJrLoaderLds>(&counters[2 * (2 * L) + 1]),
-                              ctr_ld<kJrLoaderLds>(&counters[2 * (2 * L + 1) + 1])) >= (int64_t)kHxDepth)
+      for (int w = 0; w < 21; ++w) {
+        if (P3G_DIAG_JRP == 2) {
+          he[w] = (uint32_t)x[w];
+          ho[w] = (uint32_t)(x[w] >> 32);
+        } else {
+          kp_unzip(x[w], he[w], ho[w]);
+        }
+      }
+      while (i - (int64_t)min(ctr_ld<kJrpLds>(&counters[2 * (2 * L) + 1]),
+                              ctr_ld<kJrpLds>(&counters[2 * (2 * L + 1) + 1])) >= (int64_t)kHxDepth)
         __builtin_amdgcn_s_sleep(P3G_JR_LOADER_SLEEP);
       asm volatile("" ::: "memory");
       uint32_t* slot = lring + (i % kHxDepth) * kPrSlot;
@@ -397,9 +418,9 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
         slot[w * kPrStride + 1] = ho[w];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots written before they are published
-      ctr_st<kJrLoaderLds>(&counters[2 * (2 * L)], (uint32_t)(i + 1));
-      ctr_st<kJrLoaderLds>(&counters[2 * (2 * L + 1)], (uint32_t)(i + 1));
-      if (spec_lo != nullptr) {
+      ctr_st<kJrpLds>(&counters[2 * (2 * L)], (uint32_t)(i + 1));
+      ctr_st<kJrpLds>(&counters[2 * (2 * L + 1)], (uint32_t)(i + 1));
+      if (spec_lo != nullptr && P3G_DIAG_JRP != 1) {
 #pragma unroll
         for (int w = 0; w < 21; ++w) stage[w * (kHxRows + 1) + lane] = x[w];
         pair_column_sums(stage, lane, rb + kHxRows * L, j0, nd, spec_lo, spec_cy);
@@ -410,7 +431,7 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
       const bool has = 21 * b < nd;
       uint32_t A[16];
       if (has) {
-        while ((int64_t)ctr_ld<kJrSpongeLdLds>(&counters[2 * wave]) <= b) __builtin_amdgcn_s_sleep(1);
+        while ((int64_t)ctr_ld<kJrpLds>(&counters[2 * wave]) <= b) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         const uint32_t* slot = ring + (b % kHxDepth) * kPrSlot;
 #pragma unroll
@@ -425,7 +446,7 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kPrStride + lane];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
-        ctr_st<kJrSpongeStLds>(&counters[2 * wave + 1], (uint32_t)(b + 1));
+        ctr_st<kJrpLds>(&counters[2 * wave + 1], (uint32_t)(b + 1));
       } else {
 #pragma unroll
         for (int k = 0; k < 6; ++k) carry[k] = 0u;

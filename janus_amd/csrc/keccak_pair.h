@@ -43,6 +43,15 @@ __host__ __device__ constexpr uint64_t kp_spread(uint32_t h, uint32_t p) {
 
 // Both halves of a 64-bit word at once (32-bit delta swaps, Hacker's Delight 7-2 unshuffle, on
 // each 32-bit half, then byte selects): e = kp_half(x, 0), o = kp_half(x, 1).
+// the middle-byte swap (the 8-bit delta stage): one v_perm_b32 on the device
+__host__ __device__ inline uint32_t kp_swap_mid_bytes(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(x, x, 0x03010200u);
+#else
+  const uint32_t t = (x ^ (x >> 8)) & 0x0000FF00u;
+  return x ^ t ^ (t << 8);
+#endif
+}
 __host__ __device__ inline uint32_t kp_unshuffle32(uint32_t x) {
   uint32_t t = (x ^ (x >> 1)) & 0x22222222u;
   x ^= t ^ (t << 1);
@@ -50,14 +59,11 @@ __host__ __device__ inline uint32_t kp_unshuffle32(uint32_t x) {
   x ^= t ^ (t << 2);
   t = (x ^ (x >> 4)) & 0x00F000F0u;
   x ^= t ^ (t << 4);
-  t = (x ^ (x >> 8)) & 0x0000FF00u;
-  x ^= t ^ (t << 8);
-  return x;  // even bits in the low 16, odd bits in the high 16
+  return kp_swap_mid_bytes(x);  // even bits in the low 16, odd bits in the high 16
 }
 __host__ __device__ inline uint32_t kp_shuffle32(uint32_t x) {  // the inverse
-  uint32_t t = (x ^ (x >> 8)) & 0x0000FF00u;
-  x ^= t ^ (t << 8);
-  t = (x ^ (x >> 4)) & 0x00F000F0u;
+  x = kp_swap_mid_bytes(x);
+  uint32_t t = (x ^ (x >> 4)) & 0x00F000F0u;
   x ^= t ^ (t << 4);
   t = (x ^ (x >> 2)) & 0x0C0C0C0Cu;
   x ^= t ^ (t << 2);
@@ -65,14 +71,29 @@ __host__ __device__ inline uint32_t kp_shuffle32(uint32_t x) {  // the inverse
   x ^= t ^ (t << 1);
   return x;
 }
+// low halves (lo16(a) | lo16(b) << 16) and high halves (hi16(a) | hi16(b) << 16): one v_perm_b32 each
+__host__ __device__ inline uint32_t kp_lo16s(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(b, a, 0x05040100u);
+#else
+  return (a & 0xFFFFu) | (b << 16);
+#endif
+}
+__host__ __device__ inline uint32_t kp_hi16s(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(b, a, 0x07060302u);
+#else
+  return (a >> 16) | (b & 0xFFFF0000u);
+#endif
+}
 __host__ __device__ inline void kp_unzip(uint64_t x, uint32_t& e, uint32_t& o) {
   const uint32_t u = kp_unshuffle32((uint32_t)x), v = kp_unshuffle32((uint32_t)(x >> 32));
-  e = (u & 0xFFFFu) | (v << 16);
-  o = (u >> 16) | (v & 0xFFFF0000u);
+  e = kp_lo16s(u, v);
+  o = kp_hi16s(u, v);
 }
 __host__ __device__ inline uint64_t kp_zip(uint32_t e, uint32_t o) {
-  const uint32_t lo = kp_shuffle32((e & 0xFFFFu) | (o << 16));
-  const uint32_t hi = kp_shuffle32((e >> 16) | (o & 0xFFFF0000u));
+  const uint32_t lo = kp_shuffle32(kp_lo16s(e, o));
+  const uint32_t hi = kp_shuffle32(kp_hi16s(e, o));
   return ((uint64_t)hi << 32) | lo;
 }
 
