@@ -148,10 +148,15 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
  *   "query_overlap" 1: the snapshot-mode helper query regenerates half-chunk i + 1 on a second
  *                   stream while half-chunk i is queried (two scratch halves); 0 (default): in
  *                   turn
- *   "wave_prio"     1: FixedPoint chain waves (k_helper_xof, k_jr_ring) issue at s_setprio 3 and
- *                   the FixedPoint matrix-core wire passes at 2 over co-running waves; 0: all at 0
+ *   "wave_prio"     1: FixedPoint chain waves (k_helper_xof, k_jr_ring; the lane-pair kernels'
+ *                   sponge waves only) issue at s_setprio 3 and the FixedPoint matrix-core wire
+ *                   passes at 2 over co-running waves; 2: also the lane-pair kernels' storer /
+ *                   loader waves; 0: all at 0
  *   "jr_ring"       1: FixedPoint leader joint-rand part via k_jr_ring; 0: k_jr
- *   "chain_pairs"   64-report chains per k_helper_xof / k_jr_ring workgroup: 1, 2, or 0 (auto,
+ *   "pair_chains"   1: the FixedPoint chains (k_helper_xof_pair, k_jr_ring_pair) keep each
+ *                   sponge state on a lane pair, bit-interleaved (half the instructions on the
+ *                   latency-bound chain; 64 / 128 reports per workgroup); 0: one lane per state
+ *   "chain_pairs"   (pair_chains 0) 64-report chains per k_helper_xof / k_jr_ring workgroup: 1, 2, or 0 (auto,
  *                   default: 2 once the launch would take more than half the CUs, so a leader's
  *                   and a helper's launches side by side keep one sponge wave per SIMD)
  *   "spread"        1: latency-bound sponge launches take one CU per workgroup
