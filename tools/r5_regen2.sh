@@ -1,6 +1,7 @@
 #!/bin/bash
 # config E 10,240 lane-pair chains: k_fpv_regen with and without its row stores (timing-only
-# build rgn1), and snap_chunk 384 vs 256
+# build rgn1, -DP3G_DIAG_REGEN=1: the row stores replaced by an XOR fold -- it ran 401 vs 231 ms,
+# inconclusive, and the macro was removed), and snap_chunk 384 vs 256
 set -o pipefail
 O=gpurun_out/r5_regen2; mkdir -p $O
 run() {  # name chunk
