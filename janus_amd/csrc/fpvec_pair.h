@@ -31,6 +31,19 @@ constexpr bool kJrpLds = P3G_JRP_CTR_LDS != 0;
 #define P3G_DIAG_JRP 0
 #endif
 
+// The ring counters are LDS words written with ds_write after the slot accesses they publish, and
+// one wave's LDS operations are performed in order: a publish needs no s_waitcnt before it, and a
+// sponge reads a slot's 21 words (the block's 16 and the next carry) in one go and releases the
+// slot at once (P3G_PAIR_NOWAIT 0: the waits of k_helper_xof / k_jr_ring, for A/B).
+#ifndef P3G_PAIR_NOWAIT
+#define P3G_PAIR_NOWAIT 1
+#endif
+#if P3G_PAIR_NOWAIT
+#define P3G_PAIR_PUBLISH_WAIT() asm volatile("" ::: "memory")
+#else
+#define P3G_PAIR_PUBLISH_WAIT() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#endif
+
 constexpr uint32_t kPrRows = 32;                 // reports per sponge wave (two lanes each)
 constexpr uint32_t kPrStride = 65;               // ring row pitch (dwords): conflict-free columns
 constexpr uint32_t kPrSlot = 21 * kPrStride;     // dwords per ring slot
@@ -216,7 +229,7 @@ __global__ void __launch_bounds__(5 * kHxRows) k_helper_xof_pair(Cfg cfg, uint32
       uint32_t* slot = ring + (i % kDepth) * kPrSlot;
 #pragma unroll
       for (int w = 0; w < 21; ++w) slot[w * kPrStride + lane] = j0 + w < nd ? s[w] : 0u;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
+      P3G_PAIR_PUBLISH_WAIT();  // slot written before it is published
       ctr_st<true>(&counters[3 * h], (uint32_t)(i + 1));
       perm = 21 * (i + 1) < nd;
     } else if (storer) {
@@ -233,7 +246,7 @@ __global__ void __launch_bounds__(5 * kHxRows) k_helper_xof_pair(Cfg cfg, uint32
         he[w] = slot[w * kPrStride];
         ho[w] = slot[w * kPrStride + 1];
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots read before they are released
+      P3G_PAIR_PUBLISH_WAIT();  // slots read before they are released
       ctr_st<true>(&counters[2], (uint32_t)(i + 1));
       ctr_st<true>(&counters[5], (uint32_t)(i + 1));
       uint64_t x[21];
@@ -276,28 +289,27 @@ __global__ void __launch_bounds__(5 * kHxRows) k_helper_xof_pair(Cfg cfg, uint32
     } else {
       const int64_t b = i;
       const bool data = 21 * b < nd;
-      uint32_t A[16];
+      uint32_t A[16], nc[6];
       if (data) {
         while ((int64_t)ctr_ld<true>(&counters[3 * h]) <= b) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         const uint32_t* slot = ring + (b % kDepth) * kPrSlot;
 #pragma unroll
         for (int w = 0; w < 16; ++w) A[w] = slot[w * kPrStride + lane];
-      } else {
 #pragma unroll
-        for (int w = 0; w < 16; ++w) A[w] = 0u;
-      }
-      jrp_absorb_pair(s, carry, A, b, nblocks, padw, padh, lasth, pre);
-      if (data) {
-        const uint32_t* slot = ring + (b % kDepth) * kPrSlot;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kPrStride + lane];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
+        for (int k = 1; k < 6; ++k) nc[k] = slot[(15 + k) * kPrStride + lane];
+        nc[0] = A[15];
+        P3G_PAIR_PUBLISH_WAIT();  // slot read before it is released
         ctr_st<true>(&counters[3 * h + 1], (uint32_t)(b + 1));
       } else {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) carry[k] = 0u;
+        for (int w = 0; w < 16; ++w) A[w] = 0u;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) nc[k] = 0u;
       }
+      jrp_absorb_pair(s, carry, A, b, nblocks, padw, padh, lasth, pre);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) carry[k] = nc[k];
     }
     if (perm) keccak_pair_x(s, ln, cfg.xof);
   }
@@ -417,7 +429,8 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
         slot[w * kPrStride] = he[w];
         slot[w * kPrStride + 1] = ho[w];
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots written before they are published
+      if (!kJrpLds) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // FLAT counters
+      P3G_PAIR_PUBLISH_WAIT();  // slots written before they are published
       ctr_st<kJrpLds>(&counters[2 * (2 * L)], (uint32_t)(i + 1));
       ctr_st<kJrpLds>(&counters[2 * (2 * L + 1)], (uint32_t)(i + 1));
       if (spec_lo != nullptr && P3G_DIAG_JRP != 1) {
@@ -429,28 +442,29 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
     } else {
       const int64_t b = i;
       const bool has = 21 * b < nd;
-      uint32_t A[16];
+      uint32_t A[16], nc[6];
       if (has) {
         while ((int64_t)ctr_ld<kJrpLds>(&counters[2 * wave]) <= b) __builtin_amdgcn_s_sleep(1);
         asm volatile("" ::: "memory");
         const uint32_t* slot = ring + (b % kHxDepth) * kPrSlot;
 #pragma unroll
         for (int w = 0; w < 16; ++w) A[w] = slot[w * kPrStride + lane];
-      } else {
 #pragma unroll
-        for (int w = 0; w < 16; ++w) A[w] = 0u;
-      }
-      jrp_absorb_pair(s, carry, A, b, nblocks, padw, padh, lasth, pre);
-      if (has) {
-        const uint32_t* slot = ring + (b % kHxDepth) * kPrSlot;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) carry[k] = slot[(15 + k) * kPrStride + lane];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before it is released
+        for (int k = 1; k < 6; ++k) nc[k] = slot[(15 + k) * kPrStride + lane];
+        nc[0] = A[15];
+        if (!kJrpLds || !P3G_PAIR_NOWAIT)  // FLAT counters: the reads must have returned
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        asm volatile("" ::: "memory");
         ctr_st<kJrpLds>(&counters[2 * wave + 1], (uint32_t)(b + 1));
       } else {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) carry[k] = 0u;
+        for (int w = 0; w < 16; ++w) A[w] = 0u;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) nc[k] = 0u;
       }
+      jrp_absorb_pair(s, carry, A, b, nblocks, padw, padh, lasth, pre);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) carry[k] = nc[k];
     }
     if (perm) keccak_pair_x(s, ln, cfg.xof);
   }
