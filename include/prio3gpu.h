@@ -145,9 +145,8 @@ int prio3gpu_ctx_set_async(prio3gpu_ctx* ctx, int on);
  *                   (FLP query, accumulation past the column sums, output shares); 0: full rows
  *   "snap_chunk"    reports per FixedPoint query / regeneration chunk (default 512; the
  *                   regenerated rows of one chunk are the only full-size helper scratch)
- *   "query_overlap" 1: the snapshot-mode helper query regenerates half-chunk i + 1 on a second
- *                   stream while half-chunk i is queried (two scratch halves); 0 (default): in
- *                   turn
+ *   "query_overlap" 1 (default): the snapshot-mode helper query regenerates half-chunk i + 1 on a
+ *                   second stream while half-chunk i is queried (two scratch halves); 0: in turn
  *   "wave_prio"     1: FixedPoint chain waves (k_helper_xof, k_jr_ring; the lane-pair kernels'
  *                   sponge waves only) issue at s_setprio 3 and the FixedPoint matrix-core wire
  *                   passes at 2 over co-running waves; 2: also the lane-pair kernels' storer /

@@ -220,9 +220,10 @@ struct prio3gpu_ctx {
   // k_helper_xof_pair, k_jr_ring_pair; half the instructions on the latency-bound chain)
   bool pair_chains = true;
   // "query_overlap": snapshot-mode helper query regenerates half-chunk i+1 on a second stream
-  // while half-chunk i is queried (two scratch halves; 0, the default: regenerate and query in
-  // turn -- measured faster: the VALU-bound regeneration starves the co-running wire passes)
-  bool query_overlap = false;
+  // while half-chunk i is queried (two scratch halves; the default since the lane-pair chains:
+  // config E 1,232 -> 1,200 ms per step at 10,240 reports, profiles/r05/pair/r5_pair8, r5_pair9;
+  // with the one-lane chains it measured 1,773 vs 1,765 ms, the regeneration starving the wires)
+  bool query_overlap = true;
   bool wires_mfma = true;    // "wires_mfma": SumVec chunk > 64 wire pass on the matrix cores
   bool wires_cols = true;    // "wires_cols": chunk <= 64 lane-per-column wire pass
   size_t expand_lds = 0;     // "expand_lds": dynamic LDS per k_expand block (occupancy cap)

@@ -456,15 +456,16 @@ def test_fpvec_helper_two_pass_path_bit_exact(name):
                                   {"pair_chains": 0, "chain_pairs": 2},
                                   {"snap_chunk": 5, "query_overlap": 1},
                                   {"snap_chunk": 1, "query_overlap": 1},
-                                  {"pair_chains": 0}, {"pair_chains": 0, "helper_snap": 0}],
+                                  {"pair_chains": 0}, {"pair_chains": 0, "helper_snap": 0},
+                                  {"snap_chunk": 5, "query_overlap": 0}],
                          ids=["snap", "snap_chunk1", "snap_chunk5", "rows", "pairs2", "overlap5",
-                              "overlap1", "unpaired", "unpaired_rows"])
+                              "overlap1", "unpaired", "unpaired_rows", "inturn5"])
 @pytest.mark.parametrize("name", ["fp16_3", "fp64_4", "fp16_300"])
 def test_fpvec_helper_snapshot_mode(name, opts):
     """Snapshot mode (helper_snap, the default): the FixedPoint helper keeps k_helper_xof's sponge
     snapshots instead of the expanded share and k_fpv_regen rewrites each query / accumulation
-    chunk's rows (in turn, or with query_overlap 1 the query's half-chunks regenerated on a
-    second stream beside the previous half-chunk's query).  Prep shares, output shares and the
+    chunk's rows (with query_overlap 1, the default, the query's half-chunks regenerated on a
+    second stream beside the previous half-chunk's query; 0: in turn).  Prep shares, output shares and the
     aggregate with a rejected row (regenerated rows summed directly) equal the oracle's, for one
     chunk, several chunks and the stored-rows mode."""
     b = batch(name)
