@@ -44,6 +44,12 @@ constexpr bool kJrpLds = P3G_JRP_CTR_LDS != 0;
 #define P3G_PAIR_PUBLISH_WAIT() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 #endif
 
+// P3G_JRP_PREFETCH 1: k_jr_ring_pair's loaders load block i + 1's share words while they unzip
+// and publish block i (0: load, wait, unzip in turn; A/B)
+#ifndef P3G_JRP_PREFETCH
+#define P3G_JRP_PREFETCH 1
+#endif
+
 constexpr uint32_t kPrRows = 32;                 // reports per sponge wave (two lanes each)
 constexpr uint32_t kPrStride = 65;               // ring row pitch (dwords): conflict-free columns
 constexpr uint32_t kPrSlot = 21 * kPrStride;     // dwords per ring slot
@@ -380,34 +386,47 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
   uint64_t* stage = reinterpret_cast<uint64_t*>(rings + 4 * kHxDepth * kPrSlot) +
                     (size_t)L * (21 * (kHxRows + 1));
   uint32_t* ring = rings + (size_t)wave * (kHxDepth * kPrSlot);  // a sponge's own ring
+  // share words [21 i, 21 i + 21) of the loader's row (zeros past the share)
+  auto load_block = [&](int64_t i, uint64_t x[21]) {
+    const int64_t j0 = 21 * i;
+    const uint8_t* src = data + 8 * j0;
+    if (j0 + 21 <= nd) {
+      if ((i & 1) == 0) {  // whole block: 16-B loads (block i starts 16-B aligned iff i even)
+#pragma unroll
+        for (int w = 0; w < 20; w += 2) {
+          const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src + 8 * w);
+          x[w] = v.x;
+          x[w + 1] = v.y;
+        }
+        x[20] = ld64(src + 160);
+      } else {
+        x[0] = ld64(src);
+#pragma unroll
+        for (int w = 1; w < 21; w += 2) {
+          const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src + 8 * w);
+          x[w] = v.x;
+          x[w + 1] = v.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < 21; ++w) x[w] = j0 + w < nd ? ld64(src + 8 * w) : 0ull;
+    }
+  };
+  uint64_t xn[21];
+  if (P3G_JRP_PREFETCH && loader) load_block(0, xn);
   const int64_t iters = loader ? nprod : nblocks;
   for (int64_t i = 0; i < iters; ++i) {
     bool perm = true;
     if (loader) {
       const int64_t j0 = 21 * i;
-      const uint8_t* src = data + 8 * j0;
       uint64_t x[21];
-      if (j0 + 21 <= nd) {
-        if ((i & 1) == 0) {
+      if (P3G_JRP_PREFETCH) {
 #pragma unroll
-          for (int w = 0; w < 20; w += 2) {
-            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src + 8 * w);
-            x[w] = v.x;
-            x[w + 1] = v.y;
-          }
-          x[20] = ld64(src + 160);
-        } else {
-          x[0] = ld64(src);
-#pragma unroll
-          for (int w = 1; w < 21; w += 2) {
-            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(src + 8 * w);
-            x[w] = v.x;
-            x[w + 1] = v.y;
-          }
-        }
+        for (int w = 0; w < 21; ++w) x[w] = xn[w];
+        if (i + 1 < iters) load_block(i + 1, xn);  // in flight under this block's work
       } else {
-#pragma unroll
-        for (int w = 0; w < 21; ++w) x[w] = j0 + w < nd ? ld64(src + 8 * w) : 0ull;
+        load_block(i, x);
       }
       uint32_t he[21], ho[21];
 #pragma unroll
