@@ -30,6 +30,10 @@ constexpr bool kJrpLds = P3G_JRP_CTR_LDS != 0;
 #ifndef P3G_DIAG_JRP
 #define P3G_DIAG_JRP 0
 #endif
+// Timing-only diagnostic build of k_helper_xof_pair: 1 the storer neither zips nor sums columns
+#ifndef P3G_DIAG_HXP
+#define P3G_DIAG_HXP 0
+#endif
 
 // The ring counters are LDS words written with ds_write after the slot accesses they publish, and
 // one wave's LDS operations are performed in order: a publish needs no s_waitcnt before it, and a
@@ -257,8 +261,9 @@ __global__ void __launch_bounds__(5 * kHxRows) k_helper_xof_pair(Cfg cfg, uint32
       ctr_st<true>(&counters[5], (uint32_t)(i + 1));
       uint64_t x[21];
 #pragma unroll
-      for (int w = 0; w < 21; ++w) x[w] = kp_zip(he[w], ho[w]);
-      if (spec_lo != nullptr) {
+      for (int w = 0; w < 21; ++w)
+        x[w] = P3G_DIAG_HXP == 1 ? ((uint64_t)ho[w] << 32) | he[w] : kp_zip(he[w], ho[w]);
+      if (spec_lo != nullptr && P3G_DIAG_HXP != 1) {
 #pragma unroll
         for (int w = 0; w < 21; ++w) stage[w * (kHxRows + 1) + lane] = x[w];
         // this wave's own LDS writes complete before its reads below (in-order LDS)
