@@ -120,6 +120,45 @@ class EpochPartials:
         return out
 
 
+class OrdShardStore:
+    """The batch-aggregation shards of Janus's datastore, as the patched Janus uses them with one
+    process per GPU ("The contract the Janus binding runs"): no collective.
+
+    * `flush` is `Accumulator::flush_to_datastore` (accumulator.rs:133-215) for one batch
+      identifier: the job's aggregation goes to shard `ord` (drawn by the writer in
+      [0, shard_count), accumulator.rs:88-95); an existing shard (same batch identifier and
+      `ord`, written by any process) is `merged_with` the new one and updated, else the new one is
+      put.
+    * `collect` is `compute_aggregate_share` (aggregate_share.rs:44-80): every shard of the batch
+      identifier folded -- checksums XORed, counts summed, shares merged (mod p).
+
+    The store is the shared medium (Janus's Postgres); `tests/test_multirank_cpu.py` feeds it the
+    flushes of two gloo ranks."""
+
+    def __init__(self, field_size: int, shard_count: int):
+        if shard_count < 1:
+            raise ValueError("shard_count must be >= 1")
+        self.field_size = field_size
+        self.shard_count = shard_count
+        self.rows = {}  # (batch identifier, ord) -> BatchAggregation
+
+    def flush(self, key: bytes, ord_: int, ba: BatchAggregation):
+        if not 0 <= ord_ < self.shard_count:
+            raise ValueError(f"ord {ord_} outside [0, {self.shard_count})")
+        k = (bytes(key), int(ord_))
+        cur = self.rows.get(k)
+        self.rows[k] = ba if cur is None else merge_batch_aggregations(self.field_size, [cur, ba])
+
+    def shards(self, key: bytes):
+        return sorted(o for (k, o) in self.rows if k == bytes(key))
+
+    def collect(self, key: bytes) -> BatchAggregation:
+        parts = [self.rows[(bytes(key), o)] for o in self.shards(key)]
+        if not parts:
+            raise KeyError("no batch aggregations for this batch identifier")
+        return merge_batch_aggregations(self.field_size, parts)
+
+
 def epoch_merge_device(comm, vdaf, local, local_keys, epoch: int, all_gather):
     """prio3gpu_agg_epoch_merge over a device partial `local` (AggregateShares whose slot i holds
     batch identifier local_keys[i]; slots past len(local_keys) unused): returns (union keys,

@@ -1107,9 +1107,12 @@ impl LeaderBatch {
         }
     }
 
-    /// One `LeaderStoredReport`: its encoded public share and leader input share
-    /// (`get_encoded()` of the decoded values, aggregator_core/src/datastore.rs:1298-1304).  A
-    /// share of the wrong length fails the report with InvalidMessage.
+    /// One stored client report: its public share and leader input share as the datastore holds
+    /// them (`RawLeaderStoredReport`, read by the patch's `get_client_report_raw` without the
+    /// `get_decoded_with_param` of aggregator_core/src/datastore.rs:1297-1304).  The engine
+    /// validates the encodings per report: a share of the wrong length (here) or a
+    /// non-canonical field element (`prio3gpu_prepare_init`) fails that report alone with
+    /// InvalidMessage.
     pub fn push(&mut self, report_id: &[u8; 16], time: u64, public_share: &[u8],
                 leader_input_share: &[u8]) {
         let s = &self.sizes;

@@ -30,10 +30,15 @@ What the patch does (call sites by reference file:line):
                  aggregations to `Accumulator::update_aggregated`;
   * aggregator/src/aggregator/accumulator.rs:76-122  `update_aggregated` (a pre-aggregated
       BatchAggregation merged as `update` merges one report's);
+  * aggregator_core/Cargo.toml, aggregator_core/src/datastore.rs:1160-1199  the `mi355x`
+      feature and `get_client_report_raw` / `RawLeaderStoredReport`: a client report's public
+      share and leader input share as stored, not decoded (:1297-1304 decode them);
   * aggregator/src/aggregator/aggregation_job_driver.rs
       :47-100   `AggregationJobDriver::with_gpu` (a `gpu::GpuTaskCache`);
-      :317-437  the leader loop's per-report checks stay; leader_initialized (:362-401) becomes
-                one `gpu::LeaderBatch` call for the job; the response goes to
+      :141-232  the engine's tasks read their START reports through `get_client_report_raw`;
+      :317-437  the leader loop's per-report checks stay (missing report, repeated extensions);
+                leader_initialized (:362-401) becomes one `gpu::LeaderBatch` call for the job,
+                fed the stored encodings; the response goes to
                 `process_response_from_helper_gpu` (one prepare_next + accumulate);
       :688-726  the storage tail of process_response_from_helper becomes `write_step_results`,
                 shared by both paths;
@@ -50,6 +55,7 @@ PATCH = os.path.join(HERE, "janus-0.6-mi355x.patch")
 AGG = "aggregator/src/aggregator.rs"
 DRV = "aggregator/src/aggregator/aggregation_job_driver.rs"
 ACC = "aggregator/src/aggregator/accumulator.rs"
+DS = "aggregator_core/src/datastore.rs"
 
 EDITS = [
     # ---------------------------------------------------------------- Cargo feature, module
@@ -57,6 +63,11 @@ EDITS = [
      'fpvec_bounded_l2 = ["dep:fixed", "janus_core/fpvec_bounded_l2"]\n',
      'fpvec_bounded_l2 = ["dep:fixed", "janus_core/fpvec_bounded_l2"]\n'
      '# Prio3 aggregate-init on the MI355X engine (src/gpu; build.rs compiles and links it)\n'
+     'mi355x = ["janus_aggregator_core/mi355x"]\n'),
+    ("aggregator_core/Cargo.toml",
+     'test-util = ["dep:hex", "dep:sqlx", "dep:testcontainers", "janus_core/test-util", "janus_messages/test-util"]\n',
+     'test-util = ["dep:hex", "dep:sqlx", "dep:testcontainers", "janus_core/test-util", "janus_messages/test-util"]\n'
+     '# the undecoded client-report read of the MI355X leader feed (janus_aggregator/mi355x)\n'
      'mi355x = []\n'),
     ("aggregator/src/lib.rs",
      "pub mod config;\n",
@@ -540,23 +551,54 @@ type GpuOps<'a> = Option<&'a std::convert::Infallible>;
         let mut stepped_aggregations = Vec::new();
 """),
     (DRV,
-     """            // Initialize the leader's preparation state from the input share.
-            match trace_span!("VDAF preparation").in_scope(|| {
+     """        for report_aggregation in report_aggregations {
+            // Look up report.
+            let report = if let Some(report) = client_reports.get(report_aggregation.report_id()) {
 """,
-     """            #[cfg(feature = "mi355x")]
+     """        for report_aggregation in report_aggregations {
+            // MI355X: the report as stored (undecoded, `get_client_report_raw`) goes into the
+            // job's engine batch after the same per-report checks as below; the engine validates
+            // the encodings itself (a non-canonical element fails that report: InvalidMessage)
+            #[cfg(feature = "mi355x")]
             if let Some(batch) = gpu_batch.as_mut() {
+                let report = match raw_reports.remove(report_aggregation.report_id()) {
+                    Some(report) => report,
+                    None => {
+                        info!(report_id = %report_aggregation.report_id(), "Attempted to aggregate missing report (most likely garbage collected)");
+                        self.aggregate_step_failure_counter
+                            .add(1, &[KeyValue::new("type", "missing_client_report")]);
+                        report_aggregations_to_write.push(report_aggregation.with_state(
+                            ReportAggregationState::Failed(PrepareError::ReportDropped),
+                        ));
+                        continue;
+                    }
+                };
+                let mut extension_types = HashSet::new();
+                if !report
+                    .extensions
+                    .iter()
+                    .all(|extension| extension_types.insert(extension.extension_type()))
+                {
+                    info!(report_id = %report_aggregation.report_id(), "Received report with duplicate extensions");
+                    self.aggregate_step_failure_counter
+                        .add(1, &[KeyValue::new("type", "duplicate_extension")]);
+                    report_aggregations_to_write.push(report_aggregation.with_state(
+                        ReportAggregationState::Failed(PrepareError::InvalidMessage),
+                    ));
+                    continue;
+                }
                 batch.push(
-                    report.metadata().id().as_ref(),
-                    report.metadata().time().as_seconds_since_epoch(),
-                    &report.public_share().get_encoded(),
-                    &report.leader_input_share().get_encoded(),
+                    report.metadata.id().as_ref(),
+                    report.metadata.time().as_seconds_since_epoch(),
+                    &report.public_share,
+                    &report.leader_input_share,
                 );
                 gpu_reports.push((report_aggregation, report));
                 continue;
             }
 
-            // Initialize the leader's preparation state from the input share.
-            match trace_span!("VDAF preparation").in_scope(|| {
+            // Look up report.
+            let report = if let Some(report) = client_reports.get(report_aggregation.report_id()) {
 """),
     (DRV,
      """        // Construct request, send it to the helper, and process the response.
@@ -573,9 +615,9 @@ type GpuOps<'a> = Option<&'a std::convert::Infallible>;
                         Ok(ping_pong_message) => {
                             prepare_inits.push(PrepareInit::new(
                                 ReportShare::new(
-                                    report.metadata().clone(),
-                                    report.public_share().get_encoded(),
-                                    report.helper_encrypted_input_share().clone(),
+                                    report.metadata,
+                                    report.public_share,
+                                    report.helper_encrypted_input_share,
                                 ),
                                 ping_pong_message,
                             ));
@@ -907,6 +949,226 @@ type GpuOps<'a> = Option<&'a std::convert::Infallible>;
             #[cfg(feature = "mi355x")]
             gpu: None,
         })
+"""),
+    # ---------------------------------------------------------------- datastore: raw leader read
+    (DS,
+     """use tracing::error;
+use url::Url;
+""",
+     """use tracing::error;
+use url::Url;
+
+/// A leader's client report as stored, its VDAF shares NOT decoded (`mi355x` feature): the
+/// MI355X engine takes the encodings as they are and validates them per report, so the leader
+/// skips `get_decoded_with_param` (a range check and Montgomery conversion of every field
+/// element) and the re-encoding the engine call would otherwise need.
+#[cfg(feature = "mi355x")]
+#[derive(Clone, Debug)]
+pub struct RawLeaderStoredReport {
+    pub metadata: ReportMetadata,
+    pub extensions: Vec<Extension>,
+    /// `client_reports.public_share`, as stored
+    pub public_share: Vec<u8>,
+    /// `client_reports.leader_input_share`, as stored
+    pub leader_input_share: Vec<u8>,
+    pub helper_encrypted_input_share: HpkeCiphertext,
+}
+"""),
+    (DS,
+     """        .map(|row| Self::client_report_from_row(vdaf, *task_id, *report_id, row))
+        .transpose()
+    }
+""",
+     """        .map(|row| Self::client_report_from_row(vdaf, *task_id, *report_id, row))
+        .transpose()
+    }
+
+    /// `get_client_report` for the MI355X leader feed (`mi355x` feature): the same row, with the
+    /// public share and leader input share returned as stored instead of decoded
+    /// (`client_report_from_row` decodes them).  The extensions and the helper's ciphertext are
+    /// decoded as before: the driver checks the one and forwards the other.
+    #[cfg(feature = "mi355x")]
+    #[tracing::instrument(skip(self), err)]
+    pub async fn get_client_report_raw(
+        &self,
+        task_id: &TaskId,
+        report_id: &ReportId,
+    ) -> Result<Option<RawLeaderStoredReport>, Error> {
+        let stmt = self
+            .prepare_cached(
+                "SELECT
+                    client_reports.client_timestamp,
+                    client_reports.extensions,
+                    client_reports.public_share,
+                    client_reports.leader_input_share,
+                    client_reports.helper_encrypted_input_share
+                FROM client_reports
+                JOIN tasks ON tasks.id = client_reports.task_id
+                WHERE tasks.task_id = $1
+                  AND client_reports.report_id = $2
+                  AND client_reports.client_timestamp >= COALESCE($3::TIMESTAMP - tasks.report_expiry_age * '1 second'::INTERVAL, '-infinity'::TIMESTAMP)",
+            )
+            .await?;
+        self.query_opt(
+            &stmt,
+            &[
+                /* task_id */ &task_id.as_ref(),
+                /* report_id */ &report_id.as_ref(),
+                /* now */ &self.clock.now().as_naive_date_time()?,
+            ],
+        )
+        .await?
+        .map(|row| {
+            let time = Time::from_naive_date_time(&row.get("client_timestamp"));
+            let encoded_extensions: Vec<u8> = row.get("extensions");
+            let extensions: Vec<Extension> =
+                decode_u16_items(&(), &mut Cursor::new(&encoded_extensions))?;
+            let encoded_helper_input_share: Vec<u8> = row.get("helper_encrypted_input_share");
+            Ok(RawLeaderStoredReport {
+                metadata: ReportMetadata::new(*report_id, time),
+                extensions,
+                public_share: row.get("public_share"),
+                leader_input_share: row.get("leader_input_share"),
+                helper_encrypted_input_share: HpkeCiphertext::get_decoded(
+                    &encoded_helper_input_share,
+                )?,
+            })
+        })
+        .transpose()
+    }
+"""),
+
+    # ---------------------------------------------------------------- driver: raw leader read
+    (DRV,
+     """use super::error::handle_ping_pong_error;
+""",
+     """use super::error::handle_ping_pong_error;
+
+/// The undecoded client reports of a job whose VDAF the MI355X engine runs (`mi355x` feature;
+/// `()` without it, so the default build carries nothing).
+#[cfg(feature = "mi355x")]
+type RawReports = HashMap<ReportId, janus_aggregator_core::datastore::RawLeaderStoredReport>;
+#[cfg(not(feature = "mi355x"))]
+type RawReports = ();
+"""),
+    (DRV,
+     """        // Read all information about the aggregation job.
+        let (task, aggregation_job, report_aggregations, client_reports, verify_key) = datastore
+            .run_tx_with_name("step_aggregation_job_1", |tx| {
+""",
+     """        // MI355X: a task whose VDAF the engine runs reads its reports undecoded (raw_reports)
+        #[cfg(feature = "mi355x")]
+        let gpu_wanted =
+            self.gpu.is_some() && crate::gpu::engine_params(lease.leased().vdaf()).is_some();
+
+        // Read all information about the aggregation job.
+        let (task, aggregation_job, report_aggregations, client_reports, raw_reports, verify_key) =
+            datastore
+            .run_tx_with_name("step_aggregation_job_1", |tx| {
+"""),
+    (DRV,
+     """                    // Read client reports, but only for report aggregations in state START.
+                    // TODO(#224): create "get_client_reports_for_aggregation_job" datastore
+                    // operation to avoid needing to join many futures?
+                    let client_reports: HashMap<_, _> =
+                        try_join_all(report_aggregations.iter().filter_map(|report_aggregation| {
+""",
+     """                    // MI355X: the engine's tasks (Prio3, 16-byte verify keys: exactly those
+                    // `GpuTaskCache::ops_for` gives arms) read their START reports undecoded and
+                    // leave the decoded map empty
+                    #[cfg(feature = "mi355x")]
+                    let raw = gpu_wanted && verify_key.as_bytes().len() == 16;
+                    #[cfg(not(feature = "mi355x"))]
+                    let raw = false;
+                    #[cfg(feature = "mi355x")]
+                    let raw_reports: RawReports = if raw {
+                        try_join_all(
+                            report_aggregations
+                                .iter()
+                                .filter(|report_aggregation| {
+                                    matches!(
+                                        report_aggregation.state(),
+                                        &ReportAggregationState::Start
+                                    )
+                                })
+                                .map(|report_aggregation| {
+                                    tx.get_client_report_raw(
+                                        lease.leased().task_id(),
+                                        report_aggregation.report_id(),
+                                    )
+                                    .map(|rslt| {
+                                        rslt.map(|report| {
+                                            report.map(|report| {
+                                                (*report_aggregation.report_id(), report)
+                                            })
+                                        })
+                                    })
+                                }),
+                        )
+                        .await?
+                        .into_iter()
+                        .flatten()
+                        .collect()
+                    } else {
+                        HashMap::new()
+                    };
+                    #[cfg(not(feature = "mi355x"))]
+                    let raw_reports: RawReports = ();
+
+                    // Read client reports, but only for report aggregations in state START.
+                    // TODO(#224): create "get_client_reports_for_aggregation_job" datastore
+                    // operation to avoid needing to join many futures?
+                    let client_reports: HashMap<_, _> = if raw { HashMap::new() } else {
+                        try_join_all(report_aggregations.iter().filter_map(|report_aggregation| {
+"""),
+    (DRV,
+     """                        .flatten()
+                        .collect();
+
+                    Ok((
+                        Arc::new(task),
+                        aggregation_job,
+                        report_aggregations,
+                        client_reports,
+                        verify_key,
+                    ))
+""",
+     """                        .flatten()
+                        .collect()
+                    };
+
+                    Ok((
+                        Arc::new(task),
+                        aggregation_job,
+                        report_aggregations,
+                        client_reports,
+                        raw_reports,
+                        verify_key,
+                    ))
+"""),
+    (DRV,
+     """                    report_aggregations,
+                    client_reports,
+                    verify_key,
+                )
+                .await
+""",
+     """                    report_aggregations,
+                    client_reports,
+                    raw_reports,
+                    verify_key,
+                )
+                .await
+"""),
+    (DRV,
+     """        client_reports: HashMap<ReportId, LeaderStoredReport<SEED_SIZE, A>>,
+        verify_key: VerifyKey<SEED_SIZE>,
+    ) -> Result<()>
+""",
+     """        client_reports: HashMap<ReportId, LeaderStoredReport<SEED_SIZE, A>>,
+        #[allow(unused_mut, unused_variables)] mut raw_reports: RawReports,
+        verify_key: VerifyKey<SEED_SIZE>,
+    ) -> Result<()>
 """),
 ]
 

@@ -224,3 +224,75 @@ def test_epoch_merge_refuses_ranks_at_different_epochs():
     with pytest.raises(RuntimeError):
         epoch_union(3, [b"a"], lambda obj: [obj, (2, [b"b"])])
     assert epoch_union(3, [b"b", b"a"], lambda obj: [obj, (3, [b"c", b"a"])]) == [b"a", b"b", b"c"]
+
+
+# ---- the contract the Janus binding runs: per-job flushes into `ord` shards, no collective -----
+# Each rank flushes every job's per-batch-identifier aggregation into the shared datastore as the
+# patched Janus does (Accumulator::update_aggregated, then flush_to_datastore into a random shard
+# `ord`, accumulator.rs:88-95 / :133-215); collection merges the shards (aggregate_share.rs:44-80).
+# The "datastore" is janus_amd.parallel.OrdShardStore; the rows reach it over gloo.
+SHARD_COUNT = 2  # small, so both ranks write some (batch identifier, ord) rows: the merge path
+
+
+def _ord_rank_main(rank, world, port, q):
+    import random
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = random.Random(1000 + rank)  # thread_rng().gen_range(0..shard_count) of the writer
+    rows = []
+    for job in JOBS_OF[rank]:
+        for key, bas in _key_partials(range(job * JOB, (job + 1) * JOB)).items():
+            rows.append((key, rng.randrange(SHARD_COUNT), bas))
+    got = [None] * world
+    dist.all_gather_object(got, rows)  # stands in for the rows both processes write to Postgres
+    q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_ord_shard_flush_matches_single_process():
+    """Two GPU processes flush their jobs (3 and 5) into batch-aggregation shards with random
+    `ord`, without any collective; the collection-time merge of every batch identifier's shards
+    equals the single-process aggregation of all 40 reports, bit for bit, for both aggregators."""
+    from janus_amd.parallel import OrdShardStore
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ord_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p_ in procs:
+        p_.start()
+    got = dict(q.get(timeout=180) for _ in procs)
+    for p_ in procs:
+        p_.join(timeout=60)
+        assert p_.exitcode == 0
+    assert got[0] == got[1]
+    writes = got[0]
+    stores = [OrdShardStore(16, SHARD_COUNT), OrdShardStore(16, SHARD_COUNT)]
+    writers = {}
+    for rank, rows in enumerate(writes):
+        for key, ord_, bas in rows:
+            writers.setdefault((key, ord_), set()).add(rank)
+            for which in (0, 1):
+                stores[which].flush(key, ord_, bas[which])
+    # the shards were really shared: some row was written by both processes (merged_with path)
+    # and some batch identifier spans more than one shard (the collection-time merge)
+    assert any(len(w) == 2 for w in writers.values())
+    want = _key_partials(range(N_EPOCH))
+    assert any(len(stores[0].shards(k)) > 1 for k in want)
+    for which in (0, 1):
+        for key, w in want.items():
+            g = stores[which].collect(key)
+            assert g.aggregate_share == w[which].aggregate_share
+            assert g.report_count == w[which].report_count
+            assert g.checksum == w[which].checksum and g.interval == w[which].interval
+
+
+def test_ord_shard_store_rejects_out_of_range_ord():
+    from janus_amd.parallel import BatchAggregation, OrdShardStore
+    s = OrdShardStore(16, 4)
+    with pytest.raises(ValueError):
+        s.flush(b"k", 4, BatchAggregation(bytes(16), 1))
+    with pytest.raises(KeyError):
+        s.collect(b"k")

@@ -125,7 +125,8 @@ def test_patch_applies_to_the_reference(tmp_path):
         "aggregator/Cargo.toml", "aggregator/src/lib.rs", "aggregator/src/aggregator.rs",
         "aggregator/src/aggregator/accumulator.rs",
         "aggregator/src/aggregator/aggregation_job_driver.rs",
-        "aggregator/src/bin/aggregator.rs", "aggregator/src/bin/aggregation_job_driver.rs"}
+        "aggregator/src/bin/aggregator.rs", "aggregator/src/bin/aggregation_job_driver.rs",
+        "aggregator_core/Cargo.toml", "aggregator_core/src/datastore.rs"}
     for f in files:
         os.makedirs(tmp_path / os.path.dirname(f), exist_ok=True)
         shutil.copy(os.path.join(REF, f), tmp_path / f)
@@ -137,7 +138,10 @@ def test_patch_applies_to_the_reference(tmp_path):
     toml = (tmp_path / "aggregator/Cargo.toml").read_text()
     features = toml[toml.index("[features]"):]
     features = features[:features.index("\n[", 1)]
-    assert "\nmi355x = []\n" in features
+    assert '\nmi355x = ["janus_aggregator_core/mi355x"]\n' in features
+    core = (tmp_path / "aggregator_core/Cargo.toml").read_text()
+    core = core[core.index("[features]"):]
+    assert "\nmi355x = []\n" in core[:core.index("\n[", 1)]
     lib = (tmp_path / "aggregator/src/lib.rs").read_text()
     assert '#[cfg(feature = "mi355x")]\npub mod gpu;' in lib
     # every item the patch adds to a Rust file sits behind the feature: the added lines outside a
@@ -180,6 +184,7 @@ RECEIVERS = {
         "self": "AggregationJobDriver"},
     "aggregator/src/bin/aggregation_job_driver.rs": {
         "aggregation_job_driver": "AggregationJobDriver"},
+    "aggregator_core/src/datastore.rs": {},
 }
 # methods the patch adds to reference types: (type) -> {method: arity}, read from the patch
 PATCH_TYPES = {"Accumulator": "aggregator/src/aggregator/accumulator.rs",
@@ -232,3 +237,42 @@ def test_mod_rs_status_mapping_covers_prepare_error():
                    8: "InvalidMessage"}
     assert "STATUS_BATCH_COLLECTED => PrepareError::BatchCollected" in body
     assert "_ => PrepareError::VdafPrepError" in body
+
+
+@needs_ref
+def test_leader_feed_reads_reports_undecoded(tmp_path):
+    """The leader's engine batch is fed the stored encodings: a
+    `get_client_report_raw` datastore read (the columns of aggregator_core/src/datastore.rs:
+    1162-1199 without `get_decoded_with_param`, :1297-1304) behind the feature, called by the job
+    step for the engine's tasks, whose rows go to `LeaderBatch::push` as they are -- no
+    decode/re-encode of the 135 KB SumVec leader share in Rust."""
+    added = patch_files()
+    ds = "\n".join(added["aggregator_core/src/datastore.rs"])
+    drv = "\n".join(added["aggregator/src/aggregator/aggregation_job_driver.rs"])
+    # the accessor and its row type, both behind the feature
+    assert re.search(r'#\[cfg\(feature = "mi355x"\)\]\n#\[derive\(Clone, Debug\)\]\n'
+                     r'pub struct RawLeaderStoredReport \{', ds)
+    fields = set(re.findall(r"^    pub (\w+):", ds[ds.index("pub struct RawLeaderStoredReport"):],
+                            re.M))
+    assert fields == {"metadata", "extensions", "public_share", "leader_input_share",
+                      "helper_encrypted_input_share"}
+    acc = ds[ds.index("pub async fn get_client_report_raw("):]
+    assert '#[cfg(feature = "mi355x")]' in ds[:ds.index("pub async fn get_client_report_raw(")]
+    assert len(split_args(paren_body(acc, acc.index("(")))) == 3  # &self, task_id, report_id
+    if "\n    }\n" in acc:  # (the diff may share the closing lines with the previous fn)
+        acc = acc[:acc.index("\n    }\n")]
+    assert "get_decoded_with_param" not in acc
+    assert 'public_share: row.get("public_share")' in acc
+    assert 'leader_input_share: row.get("leader_input_share")' in acc
+    # the job step reads through it and pushes the raw rows; the decoded read is skipped
+    assert "tx.get_client_report_raw(" in drv
+    assert "let client_reports: HashMap<_, _> = if raw { HashMap::new() } else {" in drv
+    push = drv[drv.index("batch.push("):]
+    push = paren_body(push, push.index("("))
+    assert split_args(push)[2:] == ["&report.public_share", "&report.leader_input_share"]
+    assert "leader_input_share().get_encoded()" not in drv
+    # every field the driver reads from a raw report exists
+    used = set(re.findall(r"\breport\.(\w+)\b(?!\s*\()", drv))
+    assert used <= fields, used - fields
+    # LeaderBatch::push takes (report id, time, public share, leader input share)
+    assert impl_methods(open(MOD).read())["LeaderBatch"]["push"] == 4
