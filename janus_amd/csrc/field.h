@@ -250,12 +250,8 @@ DEVI F128 sqn128(F128 x, int n) {
   for (int i = 0; i < n; ++i) x = Field128Ops::mul(x, x);
   return x;
 }
-#ifndef P3G_DIAG_NOINV
-#define P3G_DIAG_NOINV 0  // diagnostic build (timing only, wrong bytes): the inverse is x itself
-#endif
 DEVI F128 inv_mont128(const F128& x) {
   using FO = Field128Ops;
-  if (P3G_DIAG_NOINV) return x;
   if (!P3G_INV_EXP) {
     F128 y;
     inv128::inverse(x.w, y.w);

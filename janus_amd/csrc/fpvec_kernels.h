@@ -76,13 +76,6 @@ DEVI void jrp_absorb(uint64_t s[25], const uint64_t carry[6], const uint64_t A[1
   }
 }
 
-// Timing-only diagnostic builds of k_helper_xof (wrong bytes; tools/build_variant.sh):
-//   1: the storer waves leave at once (the producer does not wait for them)
-//   2: the consumer waves skip their permutation     3: the producer waves skip theirs
-//   4: the producer writes no ring slot               5: the producer stores no snapshot
-#ifndef P3G_DIAG_HX
-#define P3G_DIAG_HX 0
-#endif
 
 
 // Ring counters in LDS.  kLds: read and written with ds instructions; else through a volatile
@@ -199,10 +192,6 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
   const uint32_t r0 = (blockIdx.x * kPairs + pair) * kHxRows;
   if (r0 >= n) return;  // a whole pair past the batch (no barrier follows)
   if (cfg.wave_prio) __builtin_amdgcn_s_setprio(3);  // the chain first on its SIMD
-  if (P3G_DIAG_HX == 1 && storer) {
-    ctr_st<kHxLds>(vstor, 0x7FFFFFFFu);
-    return;
-  }
   const uint32_t r = r0 + lane;
   const bool live = r < n && (!status || status[r] == ST_OK);
   const uint32_t rr = r < n ? r : n - 1u;  // every lane runs the loop, clamped row
@@ -239,7 +228,7 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
     bool perm = true;
     if (producer) {
       const int64_t j0 = 21 * i;
-      if (P3G_DIAG_HX != 5 && snaps != nullptr && (i % kSnapEvery) == 0 && r < n) {
+      if (snaps != nullptr && (i % kSnapEvery) == 0 && r < n) {
         uint64_t* sp = snaps + ((size_t)r * snap_count(cfg) + (size_t)(i / kSnapEvery)) * 25;
 #pragma unroll
         for (int w = 0; w < 25; ++w) sp[w] = s[w];
@@ -248,10 +237,8 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
         __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");
       uint64_t* slot = ring + (i % kDepth) * kSlot;
-      if (P3G_DIAG_HX != 4) {
 #pragma unroll
-        for (int w = 0; w < 21; ++w) slot[w * kStride + lane] = j0 + w < nd ? s[w] : 0ull;
-      }
+      for (int w = 0; w < 21; ++w) slot[w * kStride + lane] = j0 + w < nd ? s[w] : 0ull;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot written before it is published
       ctr_st<kHxProdStLds>(vprod, (uint32_t)(i + 1));
       perm = 21 * (i + 1) < nd;
@@ -351,8 +338,6 @@ __global__ void __launch_bounds__(3 * kHxRows * kPairs) k_helper_xof(Cfg cfg, ui
         for (int k = 0; k < 6; ++k) carry[k] = 0ull;
       }
     }
-    if (P3G_DIAG_HX == 2 && !producer) perm = false;
-    if (P3G_DIAG_HX == 3 && producer) perm = false;
     if (perm) keccak_x(s, cfg.xof);
   }
   if (storer) {

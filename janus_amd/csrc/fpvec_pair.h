@@ -25,15 +25,6 @@ namespace p3g {
 #define P3G_JRP_CTR_LDS 1
 #endif
 constexpr bool kJrpLds = P3G_JRP_CTR_LDS != 0;
-// Timing-only diagnostic builds of k_jr_ring_pair (wrong bytes): 1 the loader sums no columns,
-// 2 the loader writes the raw word halves instead of unzipping them
-#ifndef P3G_DIAG_JRP
-#define P3G_DIAG_JRP 0
-#endif
-// Timing-only diagnostic build of k_helper_xof_pair: 1 the storer neither zips nor sums columns
-#ifndef P3G_DIAG_HXP
-#define P3G_DIAG_HXP 0
-#endif
 
 // The ring counters are LDS words written with ds_write after the slot accesses they publish, and
 // one wave's LDS operations are performed in order: a publish needs no s_waitcnt before it, and a
@@ -262,8 +253,8 @@ __global__ void __launch_bounds__(5 * kHxRows) k_helper_xof_pair(Cfg cfg, uint32
       uint64_t x[21];
 #pragma unroll
       for (int w = 0; w < 21; ++w)
-        x[w] = P3G_DIAG_HXP == 1 ? ((uint64_t)ho[w] << 32) | he[w] : kp_zip(he[w], ho[w]);
-      if (spec_lo != nullptr && P3G_DIAG_HXP != 1) {
+        x[w] = kp_zip(he[w], ho[w]);
+      if (spec_lo != nullptr) {
 #pragma unroll
         for (int w = 0; w < 21; ++w) stage[w * (kHxRows + 1) + lane] = x[w];
         // this wave's own LDS writes complete before its reads below (in-order LDS)
@@ -435,14 +426,7 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
       }
       uint32_t he[21], ho[21];
 #pragma unroll
-      for (int w = 0; w < 21; ++w) {
-        if (P3G_DIAG_JRP == 2) {
-          he[w] = (uint32_t)x[w];
-          ho[w] = (uint32_t)(x[w] >> 32);
-        } else {
-          kp_unzip(x[w], he[w], ho[w]);
-        }
-      }
+      for (int w = 0; w < 21; ++w) kp_unzip(x[w], he[w], ho[w]);
       while (i - (int64_t)min(ctr_ld<kJrpLds>(&counters[2 * (2 * L) + 1]),
                               ctr_ld<kJrpLds>(&counters[2 * (2 * L + 1) + 1])) >= (int64_t)kHxDepth)
         __builtin_amdgcn_s_sleep(P3G_JR_LOADER_SLEEP);
@@ -457,7 +441,7 @@ __global__ void __launch_bounds__(6 * kHxRows) k_jr_ring_pair(Cfg cfg, uint32_t 
       P3G_PAIR_PUBLISH_WAIT();  // slots written before they are published
       ctr_st<kJrpLds>(&counters[2 * (2 * L)], (uint32_t)(i + 1));
       ctr_st<kJrpLds>(&counters[2 * (2 * L + 1)], (uint32_t)(i + 1));
-      if (spec_lo != nullptr && P3G_DIAG_JRP != 1) {
+      if (spec_lo != nullptr) {
 #pragma unroll
         for (int w = 0; w < 21; ++w) stage[w * (kHxRows + 1) + lane] = x[w];
         pair_column_sums(stage, lane, rb + kHxRows * L, j0, nd, spec_lo, spec_cy);

@@ -147,16 +147,6 @@ struct Xof {
 constexpr Xof kXofShake128{1u, 0x1Fu};
 constexpr Xof kXofTurboShake128{0u, 0x01u};
 
-// P3G_KECCAK_ASM: the rounds as generated inline assembly with VGPR-bank-aware registers
-// (keccak_asm.h, tools/gen_keccak_asm.py) instead of keccak_round32 above; 1 unrolled, 2 a loop
-// of two-round bodies (~3 KB of code per call site instead of ~35 KB).
-#ifndef P3G_KECCAK_ASM
-#define P3G_KECCAK_ASM 0
-#endif
-#if P3G_KECCAK_ASM
-#include "keccak_asm.h"
-#endif
-
 DEVI void keccak_x(uint64_t a[25], const Xof& x) {
   uint32_t l[25], h[25];
 #pragma unroll
@@ -164,15 +154,8 @@ DEVI void keccak_x(uint64_t a[25], const Xof& x) {
     l[i] = (uint32_t)a[i];
     h[i] = (uint32_t)(a[i] >> 32);
   }
-#if P3G_KECCAK_ASM == 2
-  keccak_asm_rolled(l, h, x.full != 0u);
-#elif P3G_KECCAK_ASM
-  if (x.full) keccak_asm_rounds_0_12(l, h);
-  keccak_asm_rounds_12_24(l, h);
-#else
   if (x.full) keccak_rounds32<0, 12>(l, h);
   keccak_rounds32<12, 24>(l, h);
-#endif
 #pragma unroll
   for (int i = 0; i < 25; ++i) a[i] = ((uint64_t)h[i] << 32) | l[i];
 }

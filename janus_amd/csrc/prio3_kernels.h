@@ -111,49 +111,9 @@ struct SqueezeVec;
 // exact per-element path (prio's rejection sampling), so the output is the same either way.
 DEVI bool hi_ok(uint64_t hi) { return hi < 0xFFFFFFFFFFFFFFE4ull; }
 
-// Diagnostic builds (tools/build_variant.sh + tools/sponge_ab.py; wrong bytes, timing only):
-//   P3G_DIAG_EXPAND_NOSTORE  the fast squeeze folds each block into a register instead of storing
-//   P3G_DIAG_EXPAND_FIXED    the fast squeeze stores every block over the row's first 176 bytes
-//   P3G_DIAG_EXPAND_TILED    k_expand writes the meas share as element-major 64-report tiles
-//   P3G_DIAG_JR_NOLOAD       k_jr issues no LDS-DMA window fills (absorbs whatever LDS holds)
-//   P3G_DIAG_JR_NOWAIT       k_jr reads its window without waiting for the fill (stale bytes)
-//   P3G_DIAG_JR_NOABSORB     k_jr absorbs constants instead of reading its LDS window
-#ifndef P3G_DIAG_EXPAND_NOSTORE
-#define P3G_DIAG_EXPAND_NOSTORE 0
-#endif
-#ifndef P3G_DIAG_EXPAND_FIXED
-#define P3G_DIAG_EXPAND_FIXED 0
-#endif
-#ifndef P3G_DIAG_EXPAND_TILED
-#define P3G_DIAG_EXPAND_TILED 0
-#endif
-#ifndef P3G_DIAG_JR_NOLOAD
-#define P3G_DIAG_JR_NOLOAD 0
-#endif
-#ifndef P3G_DIAG_JR_NOWAIT
-#define P3G_DIAG_JR_NOWAIT 0
-#endif
-#ifndef P3G_DIAG_JR_NOABSORB
-#define P3G_DIAG_JR_NOABSORB 0
-#endif
-//   P3G_DIAG_SQ_NOLOAD       the paired Sum query issues no LDS-DMA operand fills (compute only)
-#ifndef P3G_DIAG_SQ_NOLOAD
-#define P3G_DIAG_SQ_NOLOAD 0
-#endif
-//   P3G_DIAG_FW_NOLOAD       k_flp_weights issues no gadget-coefficient fills and no weight flushes
-#ifndef P3G_DIAG_FW_NOLOAD
-#define P3G_DIAG_FW_NOLOAD 0
-#endif
-//   P3G_DIAG_FW_PHASE        k_flp_weights without the products of one phase (1 forward prefix,
-//                            2 Horner, 3 backward) -- where its time goes
-#ifndef P3G_DIAG_FW_PHASE
-#define P3G_DIAG_FW_PHASE 0
-#endif
-
 template <>
 struct SqueezeVec<Field128Ops> {
-  // ESTR: bytes from one output element to the next: 16 (a report's row) or 1024 (element-major
-  // 64-report tiles, where a wave's lanes store one contiguous 1 KB per element).
+  // ESTR: bytes from one output element to the next (16: a report's row).
   // PRE: the state holds the absorbed (unpermuted) message block; every block's permutation,
   // the first included, runs at the top of the one loop (a single Keccak copy per call site).
   template <class Next, uint32_t ESTR = 16, bool PRE = false>
@@ -162,9 +122,6 @@ struct SqueezeVec<Field128Ops> {
     uint32_t cnt = 0;
     uint32_t parity = 0;
     uint64_t carry = 0;
-#if P3G_DIAG_EXPAND_NOSTORE
-    uint64_t sink = 0;
-#endif
     while (true) {
       if constexpr (PRE) next(s);
       bool fast = !exact && cnt + 11u <= n;
@@ -177,19 +134,7 @@ struct SqueezeVec<Field128Ops> {
         for (int k = 0; k < 10; ++k) fast &= hi_ok(s[2 * k + 2]);
       }
       if (fast) {
-#if P3G_DIAG_EXPAND_FIXED  // diagnostic: every block's stores hit the row's first 176 bytes
-        uint8_t* o = out + (size_t)(parity * 16u);
-#else
         uint8_t* o = out + (size_t)cnt * ESTR;
-#endif
-#if P3G_DIAG_EXPAND_NOSTORE  // diagnostic build only (tools/sponge_ab.py): fold instead of storing
-        if (true) {
-#pragma unroll
-          for (int k = 0; k < 21; ++k) sink ^= s[k];
-          carry = s[20];
-          cnt += parity == 0 ? 10u : 11u;
-        } else
-#endif
         if (parity == 0) {
 #pragma unroll
           for (int k = 0; k < 10; ++k)
@@ -235,9 +180,6 @@ struct SqueezeVec<Field128Ops> {
       parity ^= 1u;
       if constexpr (!PRE) next(s);
     }
-#if P3G_DIAG_EXPAND_NOSTORE
-    st64(out, sink);
-#endif
   }
 };
 
@@ -440,7 +382,7 @@ __global__ void __launch_bounds__(256, P3G_EXPAND_WAVES) k_expand(Cfg cfg, uint3
 #ifndef P3G_EXPAND_ONECOPY
 #define P3G_EXPAND_ONECOPY 1
 #endif
-#if P3G_EXPAND_ONECOPY && !P3G_DIAG_EXPAND_TILED
+#if P3G_EXPAND_ONECOPY
   // proof share, then measurement share, through ONE loop body: the absorb permutation runs inside
   // the squeeze loop (PRE), so the kernel holds one copy of the unrolled permutation, not four
   uint32_t ph = 0;
@@ -464,14 +406,6 @@ __global__ void __launch_bounds__(256, P3G_EXPAND_WAVES) k_expand(Cfg cfg, uint3
 #endif
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_PROOF_SHARE, ld64(hs + 16), ld64(hs + 24), agg_id,
                              cfg.proof_len, out_proof.at(r), cfg.xof, cfg.exact_squeeze);
-#if P3G_DIAG_EXPAND_TILED  // diagnostic: element-major 64-report tiles (consumers not adapted)
-  if constexpr (FO::ES == 16) {
-    uint8_t* t = out_meas.base + (size_t)(r >> 6) * 64u * out_meas.stride + (r & 63u) * 16u;
-    xof_expand_byte_binder<FO, 1024>(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8),
-                                     agg_id, cfg.meas_len, t, cfg.xof, cfg.exact_squeeze);
-    return;
-  }
-#endif
   xof_expand_byte_binder<FO>(cfg.algo_id, DST_MEASUREMENT_SHARE, ld64(hs), ld64(hs + 8), agg_id,
                              cfg.meas_len, out_meas.at(r), cfg.xof, cfg.exact_squeeze);
 }
@@ -556,8 +490,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     const uint32_t wrap = t >= 11u ? 1u : 0u;
     const uint32_t row = min(la + cq + wrap, rlim);
     const uint32_t k = t - 11u * wrap;
-    if (!P3G_DIAG_JR_NOLOAD)
-      __builtin_amdgcn_global_load_lds(
+    __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(src + (row * mstride + 16u * k)),
           (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, 0, 0);
   };
@@ -572,8 +505,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     for (int q = 0; q < 11; ++q) {
       const uint32_t cq = (64u * q) / 11u, dq = (64u * q) % 11u;
       const uint32_t vo = lo + (lb + dq >= 11u ? wdelta : 0u);
-      if (!P3G_DIAG_JR_NOLOAD)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rs, (__attribute__((address_space(3))) void*)(win + 1024 * q), 16, vo,
             cq * mstride + 16u * dq, 0, 0);
     }
@@ -593,23 +525,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
   for (int i = 0; i < 25; ++i) s[i] = 0ull;
   for (int64_t b = 0; b < nblocks; ++b) {
     if (is_fast(b)) {
-      if (!P3G_DIAG_JR_NOWAIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // the lane index re-read per block (2 VALU): nothing lane-derived stays live across the
       // permutation, so the window and column-sum addresses need no spill slots
       uint32_t ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
       const uint64_t* L = reinterpret_cast<const uint64_t*>(win + ln * kJrWin);
-      if (P3G_DIAG_JR_NOABSORB) {
-#pragma unroll
-        for (int w = 0; w < 21; ++w) s[w] ^= (uint64_t)b * 0x9E3779B97F4A7C15ull + w;
-      } else {
       uint64_t prev = L[0];
 #pragma unroll
       for (int w = 0; w < 21; ++w) {
         const uint64_t cur = L[w + 1];
         s[w] ^= (prev >> 48) | (cur << 16);
         prev = cur;
-      }
       }
       if (spec_lo != nullptr) {
         // Speculative accumulation: column sums of the window's 21 new words over the wave's 64
@@ -1027,7 +954,6 @@ DEVI void sum_query_pair(const Cfg& cfg, uint32_t n, uint32_t r0w, uint32_t lane
       const uint8_t* pr = proof.base + (size_t)row * proof.stride;
       const uint8_t* xr = meas.base + (size_t)row * meas.stride;
       const uint32_t off[4] = {e, e + m, e + h, (uint32_t)min(e + h + m, gp_len - 1u)};
-      if (P3G_DIAG_SQ_NOLOAD) continue;
 #pragma unroll
       for (uint32_t s = 0; s < 4; ++s)
         __builtin_amdgcn_global_load_lds(
@@ -1503,7 +1429,6 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
       const uint32_t u = (ln & 7u) ^ ((q >> 1) & 7u);
       const uint32_t row = min(r0w + q, n - 1u);
       const uint32_t e = arity + min(kFwChunk * ch + u, gp_len - 1u);
-      if (P3G_DIAG_FW_NOLOAD) continue;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(proof.base + (size_t)row * proof.stride +
                                                           16u * e),
@@ -1520,7 +1445,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
     for (uint32_t i = 0; i < 8; ++i) {
       const uint32_t q = 8u * i + ql;
       const T x = FO::load(w + 16u * (8u * q + (u ^ ((q >> 1) & 7u))));
-      if (!P3G_DIAG_FW_NOLOAD && u < cnt && ((livemask >> q) & 1ull))
+      if (u < cnt && ((livemask >> q) & 1ull))
         FO::store(wm.el(r0w + q, pos + u), x);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1542,12 +1467,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
     if (k <= C && ((k - 1u) & 7u) == 0u) FO::store(S((k - 1u) >> 3), P);
     const T d = FO::sub(tm, ld_tw<FO>(cfg, k <= C ? k : 1u));
     T nP, nrp;
-#if P3G_DIAG_FW_PHASE == 1  // timing only: no forward products
-    nP = FO::add(P, d);
-    nrp = FO::add(rp, rm);
-#else
     mont_mul2(P, d, nP, rp, rm, nrp);
-#endif
     if (k <= C) P = nP;
     if (k <= c) {
       rp = nrp;
@@ -1588,13 +1508,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
         c1 = xb[u];
       } else {
         T n2, n1, n0;
-#if P3G_DIAG_FW_PHASE == 2  // timing only: no Horner products
-        n2 = FO::add(A2, t3);
-        n1 = FO::add(A1, t3);
-        n0 = FO::add(A0, t3);
-#else
         mul3<FO>(A2, t3, A1, t3, A0, t3, n2, n1, n0);
-#endif
         A2 = FO::add(n2, c2);
         A1 = FO::add(n1, c1);
         A0 = FO::add(n0, xb[u]);
@@ -1654,15 +1568,7 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
         // the chain step {inv pt_k, inv d_k}, the next entry's P_(k-2) alpha^(k-1)/m,
         // q <- q / r^c, and MM of the previous entry (k + 1)
         T lk, ninv, nptw, nq, mmp;
-#if P3G_DIAG_FW_PHASE == 3  // timing only: no backward products
-        lk = FO::add(inv, ptw);
-        ninv = FO::add(inv, d);
-        nptw = FO::add(pn, tn);
-        nq = FO::add(q, rcinv);
-        mmp = FO::add(lkp, qp);
-#else
         mont_mul5(inv, ptw, lk, inv, d, ninv, pn, tn, nptw, q, rcinv, nq, lkp, qp, mmp);
-#endif
         if ((uint32_t)u + 1u < nb) emit_mm((uint32_t)u + 1u, mmp);
         inv = ninv;
         ptw = nptw;

@@ -1,6 +1,6 @@
-"""tools/gen_keccak_asm.py's bank-aware inline-assembly Keccak-f[1600] (janus_amd/csrc/keccak_asm.h,
-the P3G_KECCAK_ASM=1 A/B build): the committed instructions, interpreted on 32-bit integers, equal a
-plain Keccak-f[1600], which is itself pinned by hashlib's SHAKE128."""
+"""tools/gen_keccak_asm.py's bank-aware inline-assembly Keccak-f[1600] (a round-5 A/B study, measured
+no faster and not part of the engine): the generated instructions, interpreted on
+32-bit integers, equal a plain Keccak-f[1600], which is itself pinned by hashlib's SHAKE128."""
 import hashlib
 import importlib.util
 import os
@@ -25,7 +25,10 @@ def test_reference_keccak_matches_shake128():
     assert b"".join(x.to_bytes(8, "little") for x in out[:4]) == hashlib.shake_128(b"").digest(32)
 
 
-def test_generated_asm_is_keccak_f():
+def test_generated_asm_is_keccak_f(tmp_path):
     g = _gen()
+    out = str(tmp_path / "keccak_asm.h")
+    g.main(out)
     for seed in (1, 2, 3):
-        assert g.selftest(seed=seed)
+        assert g.selftest(path=out, seed=seed)
+        assert g.selftest_rolled(path=out, seed=seed)

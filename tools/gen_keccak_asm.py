@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generate janus_amd/csrc/keccak_asm.h: Keccak-f[1600] rounds as inline gfx950 assembly with a
+"""Generate keccak_asm.h (default build/keccak_asm.h, or --out PATH; an A/B study, not product code): Keccak-f[1600] rounds as inline gfx950 assembly with a
 VGPR-bank-aware register assignment.
 
 Why: a VALU instruction whose source operands sit in the same VGPR bank (register index mod 4)
@@ -34,7 +34,9 @@ import random
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "janus_amd", "csrc", "keccak_asm.h")
+OUT = os.path.join(ROOT, "build", "keccak_asm.h")
+if "--out" in sys.argv:
+    OUT = sys.argv[sys.argv.index("--out") + 1]
 
 RC = [0x0000000000000001, 0x0000000000008082, 0x800000000000808a, 0x8000000080008000,
       0x000000000000808b, 0x0000000080000001, 0x8000000080008081, 0x8000000000008009,
@@ -197,7 +199,8 @@ def round_asm(R_, lo, hi, iota=True):
     return ins
 
 
-def main():
+def main(path=None):
+    path = path or OUT
     best_cost, (ba, bc, br, bb) = search()
     assert best_cost <= 10, best_cost
     base = 8  # registers v8 .. : the kernel keeps v0-v7 and everything above the block
@@ -268,12 +271,12 @@ def main():
     out.append("      : P3G_KECCAK_ASM_CLOBBERS, %s, \"scc\");\n}\n" % sg)
     text = "".join(out)
     if "--check" in sys.argv:
-        cur = open(OUT).read() if os.path.exists(OUT) else ""
+        cur = open(path).read() if os.path.exists(path) else ""
         sys.exit(0 if cur == text else 1)
-    with open(OUT, "w") as f:
+    with open(path, "w") as f:
         f.write(text)
     print("wrote %s: %d instructions per 12 rounds, conflicts/half-round %d, v%d..v%d (%d temps)"
-          % (OUT, len(body), best_cost, base, top, len(temps)))
+          % (path, len(body), best_cost, base, top, len(temps)))
 
 
 if __name__ == "__main__" and "--selftest" not in sys.argv:
