@@ -117,7 +117,11 @@ uint32_t ilog2(uint32_t x) {
   return l;
 }
 
-// Grow-only device buffer; owns its allocation (freed on destruction, never copied).
+// Grow-only device buffer; owns its allocation (freed on destruction, never copied).  Every
+// per-state buffer is sized by prio3gpu_state_create, so a call on a state never grows one (a
+// hipFree inside a call would wait for the whole device); the context-level scratch grows to the
+// largest batch it has seen.  An allocation the device cannot hold is PRIO3GPU_E_CAPACITY, with
+// the HIP error cleared so the next launch check of the same context does not report it.
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -130,7 +134,17 @@ struct DevBuf {
     if (p) HIPCHK(hipFree(p));
     p = nullptr;
     cap = 0;
-    HIPCHK(hipMalloc(&p, bytes ? bytes : 16));
+    const size_t want = bytes ? bytes : 16;
+    const hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      size_t fr = 0, tot = 0;
+      (void)hipMemGetInfo(&fr, &tot);
+      set_err("device allocation of %zu bytes failed: %s (%zu of %zu bytes free)", want,
+              hipGetErrorString(e), fr, tot);
+      return e == hipErrorOutOfMemory ? PRIO3GPU_E_CAPACITY : PRIO3GPU_E_HIP;
+    }
     cap = bytes;
     return 0;
   }
@@ -804,9 +818,7 @@ int launch_prep_xof(prio3gpu_ctx* c, prio3gpu_state* st, size_t n, const uint8_t
   uint8_t* spec_cy = nullptr;
   uint32_t snd = 0, se0 = 0, se1 = 0;
   if (g.jr_len > 0 && c->speculate && spec_range(g, snd, se0, se1)) {
-    const size_t nw = (n + 63) / 64;
-    CHK(st->spec_lo.ensure(nw * snd * 8));
-    CHK(st->spec_cy.ensure(nw * snd));
+    // sized by prio3gpu_state_create for the state's capacity (no growth inside a call)
     spec_lo = reinterpret_cast<uint64_t*>(st->spec_lo.p);
     spec_cy = st->spec_cy.u8();
     st->spec_ok = true;
@@ -1444,6 +1456,7 @@ int prio3gpu_ctx_create2(int kind, uint32_t bits, uint32_t length, uint32_t chun
     return PRIO3GPU_E_HIP;
   }
   int rc = setup_cfg(c, kind, bits, length, chunk_length);
+  if (!rc) rc = c->fallback.ensure(4);  // k_helper_xof's counter: no allocation inside a call
   if (rc) {
     prio3gpu_ctx_destroy(c);
     return rc;
@@ -1510,33 +1523,70 @@ int prio3gpu_state_create(prio3gpu_ctx* c, int agg_id, size_t capacity, prio3gpu
   st->cap = capacity;
   const Cfg& g = c->cfg;
   const size_t N = capacity;
-  int rc = 0;
-  rc |= st->t.ensure(N * 16 * g.qr_len);
-  rc |= st->jr.ensure(N * 16 * std::max<uint32_t>(1, g.jr_len));
-  rc |= st->part.ensure(N * 16);
-  rc |= st->seed.ensure(N * 16);
-  rc |= st->prep.ensure(N * g.prep_share_len);
-  rc |= st->msg.ensure(N * 16);
-  rc |= st->status.ensure(N);
+  // Every buffer a call on this state may touch, sized for `capacity` reports, so no call grows
+  // one; the sum is checked against the device's free memory before anything is allocated.
+  struct Want {
+    DevBuf* b;
+    size_t bytes;
+  };
+  std::vector<Want> plan;
+  auto want = [&](DevBuf& b, size_t bytes) { plan.push_back({&b, bytes}); };
+  want(st->t, N * 16 * g.qr_len);
+  want(st->jr, N * 16 * std::max<uint32_t>(1, g.jr_len));
+  want(st->part, N * 16);
+  want(st->seed, N * 16);
+  want(st->prep, N * g.prep_share_len);
+  want(st->msg, N * 16);
+  want(st->status, N);
   if (g.kind == KIND_SUMVEC || g.kind == KIND_HISTOGRAM)
-    rc |= st->w.ensure(N * (size_t)(flp_w_len(g) + flp_scratch_len(g)) * g.es);  // rows + scratch
+    want(st->w, N * (size_t)(flp_w_len(g) + flp_scratch_len(g)) * g.es);  // rows + scratch
   if (g.kind == KIND_FPVEC) {
-    rc |= st->w.ensure(N * (size_t)fpv_w_layout(g).len * 16);
+    want(st->w, N * (size_t)fpv_w_layout(g).len * 16);
     st->fpart_rows = std::min<size_t>(N, c->snap_chunk);
-    rc |= st->fpart.ensure(st->fpart_rows * (size_t)fpv_rows(g) * g.chunk * 32);
-    rc |= st->flags.ensure(N * 4);
+    want(st->fpart, st->fpart_rows * (size_t)fpv_rows(g) * g.chunk * 32);
+    want(st->flags, N * 4);
+  }
+  {  // speculative column sums (k_jr, the FixedPoint storer waves), one row per 64 reports
+    uint32_t snd = 0, se0 = 0, se1 = 0;
+    if (g.jr_len > 0 && spec_range(g, snd, se0, se1)) {
+      const size_t nw = (N + 63) / 64;
+      want(st->spec_lo, nw * snd * 8);
+      want(st->spec_cy, nw * snd);
+    }
   }
   st->snap = g.kind == KIND_FPVEC && agg_id == 1 && c->helper_snap;
   if (agg_id == 1) {
-    if (st->snap)  // the expanded shares live as snapshots; the full rows only on the exact path
-      rc |= st->snaps.ensure(N * (size_t)snap_count(g) * kSnapBytes);
-    else
-      rc |= st->meas.ensure(N * (size_t)g.meas_len * g.es);
-    rc |= st->proof.ensure(N * (size_t)g.proof_len * g.es);
+    const size_t row = (size_t)g.meas_len * g.es;
+    if (st->snap) {
+      // the expanded shares live as snapshots; the regenerated rows of one query chunk (two
+      // half-chunks with query_overlap) are the only full-size scratch.  The full rows exist only
+      // on the exact path (a non-canonical element), which allocates them when it runs.
+      want(st->snaps, N * (size_t)snap_count(g) * kSnapBytes);
+      want(st->scratch, 2 * ((st->fpart_rows + 1) / 2) * row);
+    } else {
+      want(st->meas, N * row);
+    }
+    want(st->proof, N * (size_t)g.proof_len * g.es);
   }
-  if (rc) {
-    prio3gpu_state_destroy(st);
-    return PRIO3GPU_E_HIP;
+  size_t need = 0;
+  for (const Want& w : plan) need += w.bytes ? w.bytes : 16;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    fr = tot = 0;
+  }
+  if (tot != 0 && need > fr) {
+    set_err("a %s state of %zu reports needs %zu bytes of device memory; %zu of %zu bytes are free",
+            agg_id == 0 ? "leader" : "helper", N, need, fr, tot);
+    delete st;
+    return PRIO3GPU_E_CAPACITY;
+  }
+  for (const Want& w : plan) {
+    const int rc = w.b->ensure(w.bytes);
+    if (rc) {
+      delete st;  // DevBuf destructors free what was allocated
+      return rc;
+    }
   }
   *out = st;
   return 0;

@@ -638,3 +638,36 @@ def test_pitched_input_shares_bit_exact(name):
     for bad in (s.leader_input_share - 16, lp_pitch + 8):
         with pytest.raises(Prio3GpuError):
             ls2.set_input_pitch(bad)
+
+
+@pytest.mark.parametrize("name,capacity,opts", [("fp16_300", 10_000_000, {"helper_snap": 0}),
+                                                ("fp16_5000", 8_000_000, {}),
+                                                ("sumvec_8_1000", 3_000_000, {})],
+                         ids=["fp16_300_rows", "fp16_5000_snap", "sumvec_8_1000"])
+def test_state_beyond_device_memory_is_capacity_error(name, capacity, opts):
+    """A helper state sized past the device's HBM is refused by prio3gpu_state_create with
+    PRIO3GPU_E_CAPACITY (-4) before anything is allocated -- not a HIP out-of-memory error from a
+    call halfway through a batch -- and the same context then prepares a normal batch bit-exact
+    (every per-state buffer is sized at creation, so calls never allocate)."""
+    import torch
+    from janus_amd._lib import Prio3GpuError
+    b = batch(name)
+    v = gpu_vdaf(b)
+    for k, val in opts.items():
+        v.set_option(k, val)
+    free, total = torch.cuda.mem_get_info()
+    with pytest.raises(Prio3GpuError) as e:
+        v.new_state(1, capacity)
+    assert "(-4)" in str(e.value) and "bytes of device memory" in str(e.value), str(e.value)
+    assert torch.cuda.mem_get_info()[0] >= free - (64 << 20)  # nothing was left allocated
+    ls, hs = v.new_state(0, b.n), v.new_state(1, b.n)
+    lp, lst = v.prepare_init(ls, b.nonces, b.public, b.leader_in)
+    assert (lst == 0).all()
+    np.testing.assert_array_equal(lp, b.leader_prep)
+    hagg, lagg = v.new_aggregate(1), v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs, b.nonces, b.public, b.helper_in, lp, agg=hagg)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(msgs, b.prep_msg)
+    v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
+    assert lagg.read(0) == expected_aggregate(b, "leader")
+    assert hagg.read(0) == expected_aggregate(b, "helper")
