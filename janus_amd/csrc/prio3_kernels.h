@@ -838,9 +838,13 @@ struct WRow {
 __host__ __device__ inline uint32_t flp_w_len(const Cfg& cfg) {
   return 2 * round8(cfg.calls) + round8(cfg.chunk) + 8;
 }
+// k_flp_weights' LDS windows and backward blocks: kFwChunk elements / calls
+constexpr uint32_t kFwChunk = 4;
 // entries of k_flp_weights' element-major scratch per report: the prefix product at the start of
-// every 8-call block of the batched inversion
-__host__ __device__ inline uint32_t flp_scratch_len(const Cfg& cfg) { return (cfg.calls + 7) / 8; }
+// every kFwChunk-call block of the batched inversion
+__host__ __device__ inline uint32_t flp_scratch_len(const Cfg& cfg) {
+  return (cfg.calls + kFwChunk - 1) / kFwChunk;
+}
 
 // Wire-seed terms of column j (wire_2j, wire_2j+1 without the measurement sums): L0 s_2j and
 // L0 s_2j+1 - HL, from the proof share's seeds; `bad` if a seed is not canonical.
@@ -1363,32 +1367,35 @@ DEVI typename FO::T sel(bool c, const typename FO::T& a, const typename FO::T& b
 // FLP query, ParallelSum types, first half, one LANE per report (Field128):
 //   * Lagrange weights L_k(t) = (alpha^k/m) (t^m - 1) / (t - alpha^k), k = 0..calls, from ONE
 //     batched inversion (Montgomery's trick over d_k = t - alpha^k) whose prefix products are kept
-//     only at the start of every 8-call block (element-major scratch, 1/8 of the products) and
-//     recomputed inside a block on the way back; r^c is folded into the same inversion, so
-//     MM[k] = L_k r^(c(k-1)) comes out of the backward pass directly (descending powers);
+//     only at the start of every kFwChunk-call block (element-major scratch) and recomputed inside
+//     a block on the way back; r^c is folded into the same inversion, so MM[k] = L_k r^(c(k-1))
+//     comes out of the backward pass directly (descending powers);
 //   * RP[j] = r^(j+1) by a running product beside the prefix products;
 //   * p(t) by three Horner chains in t^3 and the gadget-output sum sum_d c_d S[d mod m] as a lazily
 //     reduced dot product, over the gadget-poly part of the proof share only (the wire seeds are
 //     read by the wire passes, which finish wire_2j = L0 s_2j + ..., see WRow);
-//   * serial chains issue as hazard-free Field128 triples (mont_mul3).
+//   * serial chains issue as hazard-free Field128 pairs / triples (mont_mul2, mont_mul3).
+// Sized for 3 waves per SIMD (<= 168 VGPRs, 8 KB of LDS per wave): a backward block of 4 calls
+// first runs its L chain (three products per step: L_k = inv P_(k-1) alpha^k/m, inv <- inv d_k and
+// the next entry's P_(k-2) alpha^(k-1)/m), parks the L_k in the output window and flushes them as
+// LM, then forms MM_k = L_k q and q <- q / r^c as pairs from the window (two products per step).
 // Table entries (alpha^k, alpha^k/m, S_i) are wave-uniform (scalar loads).  Memory moves coalesced
-// through two per-wave LDS windows of 8 elements x 64 reports (slot 8q + (u ^ ((q >> 1) & 7))
+// through two per-wave LDS windows of 4 elements x 64 reports (slot 4q + (u ^ ((q >> 2) & 3))
 // holds element u of report q: each lane's ds_read/write_b128 of its own row is bank-conflict-free,
-// and 8 lanes cover one report's 128 contiguous bytes): the proof share arrives by LDS-DMA, the
-// weight rows leave 8 entries at a time.  Per SumVec(8,1000) report it reads the 255 gadget
-// coefficients (4 KB) and writes MM, LM, RP and five scalars (4.4 KB) plus 0.2 KB of scratch.
+// and 4 lanes cover 64 contiguous bytes of one report's row): the proof share arrives by LDS-DMA,
+// the weight rows leave 4 entries (half a line; the next flush completes the line) at a time.  Per
+// SumVec(8,1000) report it reads the 255 gadget coefficients (4 KB) and writes MM, LM, RP and five
+// scalars (4.4 KB) plus 0.4 KB of scratch.
 // ------------------------------------------------------------------------------------------------
 #ifndef P3G_FLP_PRIO
 #define P3G_FLP_PRIO 0  // A/B knob: s_setprio of the FLP kernels (schedules that co-run them)
 #endif
-constexpr uint32_t kFwChunk = 8;                  // elements per LDS window
 constexpr uint32_t kFwWin = 64 * kFwChunk * 16;  // bytes per window (one wave)
 constexpr uint32_t kFwThreads = 128;
 
-__global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n, CRows proof,
-                                                            CRows tq, CRows jr, CRows part,
-                                                            Rows out_prep, uint8_t* status, WMat wm,
-                                                            uint8_t* scr) {
+__global__ void __launch_bounds__(kFwThreads) __attribute__((amdgpu_waves_per_eu(3)))
+k_flp_weights(Cfg cfg, uint32_t n, CRows proof, CRows tq, CRows jr, CRows part, Rows out_prep,
+              uint8_t* status, WMat wm, uint8_t* scr) {
   using FO = Field128Ops;
   using T = F128;
   if constexpr (P3G_FLP_PRIO > 0) __builtin_amdgcn_s_setprio(P3G_FLP_PRIO);
@@ -1405,52 +1412,55 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   const uint32_t m = cfg.m, logm = cfg.logm, C = cfg.calls, c = cfg.chunk;
   const uint32_t arity = cfg.arity, gp_len = cfg.gp_len;
   const WRow W(cfg);
-  const uint32_t sw = (lane >> 1) & 7u;  // this lane's swizzle
+  constexpr uint32_t K = kFwChunk;
+  const uint32_t sw = (lane >> 2) & (K - 1u);  // this lane's swizzle
   const T one = FO::one_mont();
   bool bad = false;
-  // block-start prefix products, element-major: entry b holds P_(8b) of report rr
+  // block-start prefix products, element-major: entry b holds P_(Kb) of report rr
   auto S = [&](uint32_t b) { return scr + ((size_t)b * n + rr) * 16u; };
   // this lane's slot u of a window.  An inline-asm ds_write: hipcc cannot tell a plain LDS store
   // from a write the earlier LDS-DMA fills might race with, and put a vmcnt(0) in front of every
   // one -- a wait for the flush's global stores (the fills themselves are waited for explicitly
   // before the window is read, and are all done before the backward pass writes win)
   auto put = [&](uint8_t* w, uint32_t u, const T& v) {
-    lds_store16(w + 128u * lane + 16u * (u ^ sw), v);
+    lds_store16(w + 16u * K * lane + 16u * (u ^ sw), v);
   };
-  // gadget-poly window <- coefficients [8 ch, 8 ch + 8) of the wave's 64 rows (LDS-DMA instruction
-  // i fills slots [64i, 64i + 64): report 8i + lane/8, element (lane & 7) ^ swizzle)
+  auto get = [&](const uint8_t* w, uint32_t u) {
+    return FO::load(w + 16u * K * lane + 16u * (u ^ sw));
+  };
+  // gadget-poly window <- coefficients [K ch, K ch + K) of the wave's 64 rows (LDS-DMA instruction
+  // i fills slots [64i, 64i + 64): report 16i + lane/4, element (lane & 3) ^ swizzle)
   auto stage = [&](uint32_t ch) {
     uint32_t ln;  // opaque copy (see flush)
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-    const uint32_t ql = ln >> 3;
+    const uint32_t ql = ln / K;
 #pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) {
-      const uint32_t q = 8u * i + ql;
-      const uint32_t u = (ln & 7u) ^ ((q >> 1) & 7u);
+    for (uint32_t i = 0; i < K; ++i) {
+      const uint32_t q = (64u / K) * i + ql;
+      const uint32_t u = (ln & (K - 1u)) ^ ((q >> 2) & (K - 1u));
       const uint32_t row = min(r0w + q, n - 1u);
-      const uint32_t e = arity + min(kFwChunk * ch + u, gp_len - 1u);
+      const uint32_t e = arity + min(K * ch + u, gp_len - 1u);
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(proof.base + (size_t)row * proof.stride +
                                                           16u * e),
           (__attribute__((address_space(3))) void*)(win + 1024u * i), 16, 0, 0);
     }
   };
-  // weight-row entries [pos, pos + cnt) (cnt <= 8) of every live report of the wave <- window w
+  // weight-row entries [pos, pos + cnt) (cnt <= K) of every live report of the wave <- window w
   auto flush = [&](uint8_t* w, uint32_t pos, uint32_t cnt) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    uint32_t ln;  // opaque copy: keeps LICM from hoisting 8 row addresses out of the callers' loops
+    uint32_t ln;  // opaque copy: keeps LICM from hoisting the row addresses out of the callers' loops
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-    const uint32_t ql = ln >> 3, u = ln & 7u;
+    const uint32_t ql = ln / K, u = ln & (K - 1u);
 #pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) {
-      const uint32_t q = 8u * i + ql;
-      const T x = FO::load(w + 16u * (8u * q + (u ^ ((q >> 1) & 7u))));
-      if (u < cnt && ((livemask >> q) & 1ull))
-        FO::store(wm.el(r0w + q, pos + u), x);
+    for (uint32_t i = 0; i < K; ++i) {
+      const uint32_t q = (64u / K) * i + ql;
+      const T x = FO::load(w + 16u * (K * q + (u ^ ((q >> 2) & (K - 1u)))));
+      if (u < cnt && ((livemask >> q) & 1ull)) FO::store(wm.el(r0w + q, pos + u), x);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
-  const uint32_t nch = (gp_len + kFwChunk - 1u) / kFwChunk;
+  const uint32_t nch = (gp_len + K - 1u) / K;
   stage(nch - 1u);  // in flight under the prefix products
 
   const T tm = FO::to_mont(FO::load(tq.at(rr)));
@@ -1459,21 +1469,21 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   for (uint32_t i = 0; i < logm; ++i) tmm = FO::mul(tmm, tmm);  // t^m
   const bool tbad = FO::eq(tmm, one);
 
-  // ---- forward: P_k = d_0 ... d_k (k <= C; P_(8b) parked for block b) beside RP[j] = r^(j+1) ----
+  // ---- forward: P_k = d_0 ... d_k (k <= C; P_(Kb) parked for block b) beside RP[j] = r^(j+1) ----
   T P = FO::sub(tm, one);  // d_0 (alpha^0 = 1)
   T rp = one;
   const uint32_t steps = C > c ? C : c;
   for (uint32_t k = 1; k <= steps; ++k) {
-    if (k <= C && ((k - 1u) & 7u) == 0u) FO::store(S((k - 1u) >> 3), P);
+    if (k <= C && ((k - 1u) & (K - 1u)) == 0u) FO::store(S((k - 1u) / K), P);
     const T d = FO::sub(tm, ld_tw<FO>(cfg, k <= C ? k : 1u));
     T nP, nrp;
     mont_mul2(P, d, nP, rp, rm, nrp);
     if (k <= C) P = nP;
     if (k <= c) {
       rp = nrp;
-      const uint32_t u = (k - 1u) & 7u;
+      const uint32_t u = (k - 1u) & (K - 1u);
       put(wout, u, rp);
-      if (u == 7u || k == c) flush(wout, W.rp((k - 1u) & ~7u), u + 1u);
+      if (u == K - 1u || k == c) flush(wout, W.rp((k - 1u) & ~(K - 1u)), u + 1u);
     }
   }
   const T rc = rp;  // r^c
@@ -1485,19 +1495,18 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   T A0 = FO::zero(), A1 = FO::zero(), A2 = FO::zero(), c2 = FO::zero(), c1 = FO::zero();
   Wide gw;
   wide_zero(gw);
-  const uint8_t* myrow = win + 128u * lane;
   for (int ch = (int)nch - 1; ch >= 0; --ch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    T xb[kFwChunk];
+    T xb[K];
 #pragma unroll
-    for (uint32_t u = 0; u < kFwChunk; ++u) xb[u] = FO::load(myrow + 16u * (u ^ sw));
+    for (uint32_t u = 0; u < K; ++u) xb[u] = get(win, u);
     if (ch > 0) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       stage((uint32_t)ch - 1u);
     }
-    const uint32_t e0 = kFwChunk * (uint32_t)ch;
+    const uint32_t e0 = K * (uint32_t)ch;
 #pragma unroll
-    for (int u = kFwChunk - 1; u >= 0; --u) {
+    for (int u = K - 1; u >= 0; --u) {
       const uint32_t e = e0 + (uint32_t)u;  // coefficient index (wave-uniform)
       if (e >= gp_len) continue;
       bad |= !FO::is_canonical(xb[u]);
@@ -1537,50 +1546,48 @@ __global__ void __launch_bounds__(kFwThreads) k_flp_weights(Cfg cfg, uint32_t n,
   const T rcinv = rz ? FO::zero() : ivP;
   T inv = FO::mul(rz ? iv : ivrc, FO::sub(tmm, one));  // (t^m - 1) / (d_0 ... d_C)
 
-  // ---- backward, k = C .. 1 in blocks of 8: L_k = inv P_(k-1) alpha^k/m, inv <- inv d_k,
-  //      MM_k = L_k (r^c)^(k-1) (q <- q / r^c).  LM leaves through wout, MM through win. ----
+  // ---- backward, k = C .. 1 in blocks of K: L_k = inv P_(k-1) alpha^k/m, inv <- inv d_k (LM
+  //      through wout), then MM_k = L_k (r^c)^(k-1), q <- q / r^c (MM through win) ----
   T lsum = FO::zero(), smm = FO::zero();
-  for (int blk = (int)((C - 1u) >> 3); blk >= 0; --blk) {
-    const uint32_t lo = 8u * (uint32_t)blk + 1u;
-    const uint32_t nb = C - lo + 1u < kFwChunk ? C - lo + 1u : kFwChunk;
-    T pb[kFwChunk];
+  for (int blk = (int)((C - 1u) / K); blk >= 0; --blk) {
+    const uint32_t lo = K * (uint32_t)blk + 1u;
+    const uint32_t nb = C - lo + 1u < K ? C - lo + 1u : K;
+    T pb[K];
     pb[0] = FO::load(S((uint32_t)blk));  // P_(lo - 1)
 #pragma unroll
-    for (uint32_t u = 1; u < kFwChunk; ++u)
+    for (uint32_t u = 1; u < K; ++u)
       if (u < nb) pb[u] = FO::mul(pb[u - 1], FO::sub(tm, ld_tw<FO>(cfg, lo + u - 1u)));
     T ptw = one;
-    // MM of an entry (L_k q) is formed one step later, beside the next entry's chain products,
-    // so every step issues five independent products (mont_mul5)
-    T lkp = FO::zero(), qp = FO::zero();
-    auto emit_mm = [&](uint32_t u, const T& mm_raw) {
-      const T mm = rz ? (lo + u == 1u ? lkp : FO::zero()) : mm_raw;
-      put(win, u, mm);
-      smm = FO::add(smm, mm);
-    };
 #pragma unroll
-    for (int u = kFwChunk - 1; u >= 0; --u) {
+    for (int u = K - 1; u >= 0; --u) {
       if ((uint32_t)u < nb) {
         const uint32_t k = lo + (uint32_t)u;
         if ((uint32_t)u + 1u == nb) ptw = FO::mul(pb[u], ld_tw<FO>(cfg, 2u * m + 1u + k));
         const T d = FO::sub(tm, ld_tw<FO>(cfg, k));
         const T pn = u > 0 ? pb[u > 0 ? u - 1 : 0] : one;
         const T tn = u > 0 ? ld_tw<FO>(cfg, 2u * m + k) : one;
-        // the chain step {inv pt_k, inv d_k}, the next entry's P_(k-2) alpha^(k-1)/m,
-        // q <- q / r^c, and MM of the previous entry (k + 1)
-        T lk, ninv, nptw, nq, mmp;
-        mont_mul5(inv, ptw, lk, inv, d, ninv, pn, tn, nptw, q, rcinv, nq, lkp, qp, mmp);
-        if ((uint32_t)u + 1u < nb) emit_mm((uint32_t)u + 1u, mmp);
+        // the chain step {inv pt_k, inv d_k} and the next entry's P_(k-2) alpha^(k-1)/m
+        T lk, ninv, nptw;
+        mul3<FO>(inv, ptw, inv, d, pn, tn, lk, ninv, nptw);
         inv = ninv;
         ptw = nptw;
-        lkp = lk;
-        qp = q;
-        q = nq;
         put(wout, (uint32_t)u, lk);
         lsum = FO::add(lsum, lk);
       }
     }
-    emit_mm(0u, FO::mul(lkp, qp));
     flush(wout, W.lm(lo - 1u), nb);
+#pragma unroll
+    for (int u = K - 1; u >= 0; --u) {
+      if ((uint32_t)u < nb) {
+        const T lk = get(wout, (uint32_t)u);
+        T mm, nq;
+        mont_mul2(lk, q, mm, q, rcinv, nq);
+        if (rz) mm = lo + (uint32_t)u == 1u ? lk : FO::zero();
+        q = nq;
+        put(win, (uint32_t)u, mm);
+        smm = FO::add(smm, mm);
+      }
+    }
     flush(win, W.mm(lo - 1u), nb);
   }
   const T l0 = FO::mul(inv, ld_tw<FO>(cfg, 2u * m + 1u));  // k = 0
