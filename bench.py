@@ -50,7 +50,7 @@ VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 # Measured register-only Keccak-f[1600] ceiling of one MI355X (tools/mb_keccak_occ.hip,
 # profiles/microbench_keccak_mem_r01.log: 10.3-10.8 G permutations/s at 2-6 waves/SIMD)
 KECCAK_CEILING = 10.8e9
-PMC_ROUND = "r05"
+PMC_ROUND = "r06"
 
 
 def cpu_threads(requested=0):
