@@ -179,7 +179,12 @@ int prio3gpu_ctx_wait_mark(prio3gpu_ctx* ctx, prio3gpu_ctx* other, int mark);
 void* prio3gpu_ctx_stream(prio3gpu_ctx* ctx);
 
 /* Preparation state + device scratch for up to `capacity` reports of one aggregator
- * (Prio3PrepareState for a whole batch). */
+ * (Prio3PrepareState for a whole batch).  Every buffer a call on the state can use is allocated
+ * here, after checking the total against the device's free memory: a state the device cannot
+ * hold is PRIO3GPU_E_CAPACITY (the message gives the bytes needed and free) with nothing
+ * allocated, and calls on a created state do not allocate (except the FixedPoint helper's exact
+ * path after a non-canonical squeezed element in snapshot mode, which allocates the full rows and
+ * also reports a failure as PRIO3GPU_E_CAPACITY). */
 int prio3gpu_state_create(prio3gpu_ctx* ctx, int agg_id, size_t capacity, prio3gpu_state** out);
 int prio3gpu_state_destroy(prio3gpu_state* st);
 /* Row pitch of the input shares this state's prepare_init / prepare_init_xof / helper_init calls
