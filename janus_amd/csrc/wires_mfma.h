@@ -39,10 +39,6 @@ namespace p3g {
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 typedef int i32x16_t __attribute__((ext_vector_type(16)));
 
-// timing-only diagnostic build (wrong bytes): no main loop
-#ifndef WM_DIAG_NOLOOP
-#define WM_DIAG_NOLOOP 0
-#endif
 #ifndef WM_PREFETCH
 #define WM_PREFETCH 1
 #endif
@@ -205,7 +201,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       acc_b[i] = 0;
     }
     uint64_t maybe = 0ull;  // lane mask: some element with top word 2^32 - 1 (exact check below)
-    for (uint32_t q0 = 0; q0 < (WM_DIAG_NOLOOP ? 0u : KQ); q0 += U) {
+    for (uint32_t q0 = 0; q0 < KQ; q0 += U) {
       if (!WM_PREFETCH || q0 > 0 || tile != wv) load_batch(tile, q0, xv);
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
