@@ -671,3 +671,39 @@ def test_state_beyond_device_memory_is_capacity_error(name, capacity, opts):
     v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
     assert lagg.read(0) == expected_aggregate(b, "leader")
     assert hagg.read(0) == expected_aggregate(b, "helper")
+
+
+@pytest.mark.parametrize("name,n", [("sumvec_8_1000", 129), ("sumvec_8_1000", 200),
+                                    ("hist256", 191), ("countvec15", 257),
+                                    ("sumvec_odd_calls", 130)])
+def test_ragged_multiwave_batches_match_c_restatement(name, n):
+    """Batches that end inside a wave and inside a block (k_flp_weights: 2 waves per block, lane
+    per report, dead lanes computing on a clamped row; k_jr / k_expand: 4 waves per block): both
+    aggregators' prep shares, the prep messages and both aggregates equal the C restatement's
+    (oracle/prio3_ref.c, itself cross-checked against the Python oracle), report for report."""
+    from oracle import prio3 as O
+    from oracle.ref import Prio3Ref
+    from janus_amd.prio3 import Prio3Gpu
+    c = CONFIGS[name]
+    vk = O.synth_verify_key(b"ragged")
+    ref = Prio3Ref(c["kind"], vk, c["bits"], c["length"], c["chunk"])
+    g = ref.gen(b"ragged-" + name.encode(), 0, n, threads=8)
+    res = ref.prepare_batch(g["nonces"], g["public"], g["leader_in"], g["helper_in"], threads=8)
+    assert (res["status"] == 0).all() and res["count"] == n
+    v = Prio3Gpu(c["kind"], vk, bits=c["bits"], length=c["length"], chunk_length=c["chunk"])
+    ls, hs = v.new_state(0, n), v.new_state(1, n)
+    lp, lst = v.prepare_init(ls, g["nonces"], g["public"], g["leader_in"])
+    assert (lst == 0).all()
+    np.testing.assert_array_equal(lp, res["lprep"])
+    hp, hst = v.prepare_init(hs, g["nonces"], g["public"], g["helper_in"])
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(hp, res["hprep"])
+    hs2 = v.new_state(1, n)
+    hagg, lagg = v.new_aggregate(1), v.new_aggregate(1)
+    msgs, hst = v.helper_init(hs2, g["nonces"], g["public"], g["helper_in"], lp, agg=hagg)
+    assert (hst == 0).all()
+    np.testing.assert_array_equal(msgs, res["msgs"])
+    v.prepare_next(ls, msgs, lst, want_output_shares=False, agg=lagg)
+    (la, lc), (ha, hc) = lagg.read(0), hagg.read(0)
+    assert lc == hc == n
+    assert la == res["agg_l"].tobytes() and ha == res["agg_h"].tobytes()
