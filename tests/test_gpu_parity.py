@@ -675,10 +675,12 @@ def test_state_beyond_device_memory_is_capacity_error(name, capacity, opts):
 
 @pytest.mark.parametrize("name,n", [("sumvec_8_1000", 129), ("sumvec_8_1000", 200),
                                     ("hist256", 191), ("countvec15", 257),
-                                    ("sumvec_odd_calls", 130)])
+                                    ("sumvec_odd_calls", 130), ("fp16_300", 130),
+                                    ("fp64_4", 200), ("sum32", 300), ("count", 1000)])
 def test_ragged_multiwave_batches_match_c_restatement(name, n):
     """Batches that end inside a wave and inside a block (k_flp_weights: 2 waves per block, lane
-    per report, dead lanes computing on a clamped row; k_jr / k_expand: 4 waves per block): both
+    per report, dead lanes computing on a clamped row; k_jr / k_expand: 4 waves per block; the
+    FixedPoint chain kernels: 64 / 128 reports per workgroup, several workgroups): both
     aggregators' prep shares, the prep messages and both aggregates equal the C restatement's
     (oracle/prio3_ref.c, itself cross-checked against the Python oracle), report for report."""
     from oracle import prio3 as O
