@@ -41,6 +41,14 @@ CONFIGS = {
     "sumvec_chunk65": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(3, 300, 65), bits=3,
                            length=300, chunk=65),
     "hist4": dict(kind=3, ctor=lambda: O.Prio3.new_histogram(4, 2), bits=0, length=4, chunk=2),
+    # ParallelSum with ONE gadget call (the batched inversion, the backward block and the MM
+    # powers at their smallest) and with three
+    "sumvec_calls1": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(1, 1, 1), bits=1, length=1,
+                          chunk=1),
+    "hist_calls1": dict(kind=3, ctor=lambda: O.Prio3.new_histogram(2, 2), bits=0, length=2,
+                        chunk=2),
+    "sumvec_calls3": dict(kind=2, ctor=lambda: O.Prio3.new_sum_vec(3, 4, 4), bits=3, length=4,
+                          chunk=4),
     "hist256": dict(kind=3, ctor=lambda: O.Prio3.new_histogram(256, 16), bits=0, length=256,
                     chunk=16),
     # FixedPointBoundedL2VecSum (Janus Prio3FixedPoint{16,32,64}BitBoundedL2VecSum { length })

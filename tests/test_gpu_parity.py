@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 SIZES = {"count": 64, "sum8": 40, "sum32": 24, "sum5": 24, "sum1": 16, "sum64": 16, "sum2": 70,
          "sum4": 70, "sum16": 70, "sumvec_small": 40, "countvec15": 24, "hist4": 40,
          "hist256": 24, "sumvec_8_1000": 6, "sumvec_odd_calls": 8, "sumvec_chunk128": 8, "sumvec_chunk65": 8, "fp16_3": 12, "fp32_5": 8, "fp64_4": 8, "fp16_300": 6,
-         "fp16_5000": 2}
+         "fp16_5000": 2, "sumvec_calls1": 8, "hist_calls1": 8, "sumvec_calls3": 8}
 FPVEC = [k for k in SIZES if k.startswith("fp")]
 
 _cache = {}
@@ -676,7 +676,9 @@ def test_state_beyond_device_memory_is_capacity_error(name, capacity, opts):
 @pytest.mark.parametrize("name,n", [("sumvec_8_1000", 129), ("sumvec_8_1000", 200),
                                     ("hist256", 191), ("countvec15", 257),
                                     ("sumvec_odd_calls", 130), ("fp16_300", 130),
-                                    ("fp64_4", 200), ("sum32", 300), ("count", 1000)])
+                                    ("fp64_4", 200), ("sum32", 300), ("count", 1000),
+                                    ("sumvec_calls1", 70), ("hist_calls1", 70),
+                                    ("sumvec_calls3", 70)])
 def test_ragged_multiwave_batches_match_c_restatement(name, n):
     """Batches that end inside a wave and inside a block (k_flp_weights: 2 waves per block, lane
     per report, dead lanes computing on a clamped row; k_jr / k_expand: 4 waves per block; the
